@@ -1,0 +1,208 @@
+"""bz2mi -- Python binding of libbz2mi (MI355X-native bzip2 block compression).
+
+Thin ctypes layer over the C ABI declared in include/bz2mi.h.  The shared
+library is built in-tree (``make -C bzip2-opencl_amd``) and always loaded from
+this directory; there is no CPU fallback -- importing works without a GPU, but
+every compression call needs the HIP device and fails loudly otherwise.
+
+Reference interface mirrored: OutputStream(std::ostream&, level, parallel)
+/ write / close (Stan1slav337/Bzip2-OpenCL include/OutputStream.hpp:65-176),
+with the same argument meaning and the same errors (ValueError for
+std::invalid_argument, RuntimeError for std::runtime_error).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbz2mi.so")
+
+BZ2MI_OK = 0
+BZ2MI_EINVAL = -1
+BZ2MI_EDEVICE = -2
+BZ2MI_ESPACE = -3
+BZ2MI_ESTATE = -4
+
+# every symbol include/bz2mi.h declares
+EXPORTS = (
+    "bz2mi_last_error", "bz2mi_device_count", "bz2mi_version", "bz2mi_create", "bz2mi_destroy",
+    "bz2mi_compress_bound", "bz2mi_compress_rle1", "bz2mi_finish", "bz2mi_compress_blocks",
+    "bz2mi_compress", "bz2mi_compress_device", "bz2mi_last_timings", "bz2mi_blocks_done",
+)
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libbz2mi.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libbz2mi.so not built: run `make -C {os.path.dirname(_HERE)}` ({LIB_PATH})")
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    L.bz2mi_last_error.restype = c.c_char_p
+    L.bz2mi_device_count.restype = c.c_int
+    L.bz2mi_version.restype = c.c_char_p
+    L.bz2mi_create.restype = c.c_void_p
+    L.bz2mi_create.argtypes = [c.c_int, c.c_int, c.c_int, c.c_int]
+    L.bz2mi_destroy.argtypes = [c.c_void_p]
+    L.bz2mi_compress_bound.restype = c.c_size_t
+    L.bz2mi_compress_bound.argtypes = [c.c_size_t, c.c_int, c.c_int]
+    L.bz2mi_compress_rle1.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_void_p, c.c_uint32,
+                                      c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t)]
+    L.bz2mi_finish.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t)]
+    L.bz2mi_compress_blocks.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_uint32, c.c_void_p,
+                                        c.c_size_t, c.c_void_p]
+    L.bz2mi_compress.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
+                                 c.POINTER(c.c_size_t)]
+    L.bz2mi_compress_device.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
+                                        c.POINTER(c.c_size_t), c.c_void_p]
+    L.bz2mi_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
+    L.bz2mi_blocks_done.restype = c.c_uint64
+    L.bz2mi_blocks_done.argtypes = [c.c_void_p]
+    for name in ("bz2mi_compress_rle1", "bz2mi_finish", "bz2mi_compress_blocks", "bz2mi_compress",
+                 "bz2mi_compress_device", "bz2mi_last_timings"):
+        getattr(L, name).restype = c.c_int
+    _lib = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc == BZ2MI_OK:
+        return
+    msg = lib().bz2mi_last_error().decode(errors="replace")
+    if rc == BZ2MI_EINVAL:
+        raise ValueError(msg)
+    raise RuntimeError(msg or f"bz2mi error {rc}")
+
+
+def compress_bound(n: int, level: int = 9, unit: int = 10000) -> int:
+    return int(lib().bz2mi_compress_bound(n, level, unit))
+
+
+def _ptr(buf) -> int:
+    """Address of a bytes-like / numpy buffer (host memory)."""
+    import numpy as np
+    a = np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+    return a.ctypes.data
+
+
+class Context:
+    """A bz2mi_ctx: one compressed stream on one device (level, p, unit)."""
+
+    def __init__(self, level: int = 9, parallel: int = 10, unit: int = 10000, device: int = 0):
+        L = lib()
+        h = L.bz2mi_create(level, parallel, unit, device)
+        if not h:
+            msg = L.bz2mi_last_error().decode(errors="replace")
+            if "Invalid" in msg:
+                raise ValueError(msg)
+            raise RuntimeError(msg)
+        self._h = h
+        self.level, self.parallel, self.unit = level, parallel, unit
+        self.block_size = level * unit
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().bz2mi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self) -> int:
+        return self._h
+
+    def compress(self, data) -> bytes:
+        """Whole stream: host RLE1 front end + device path + framing."""
+        import numpy as np
+        src = np.frombuffer(bytes(data) if not isinstance(data, (bytes, bytearray, np.ndarray)) else data,
+                            dtype=np.uint8)
+        cap = compress_bound(src.size, self.level, self.unit)
+        out = np.empty(cap, dtype=np.uint8)
+        n = ctypes.c_size_t(0)
+        _check(lib().bz2mi_compress(self._h, src.ctypes.data if src.size else None, src.size,
+                                    out.ctypes.data, cap, ctypes.byref(n)))
+        return out[: n.value].tobytes()
+
+    def compress_blocks(self, blocks: list[bytes]):
+        """Payload bits of RLE1 blocks (kernel_close analogue): list of (bytes, nbits)."""
+        import numpy as np
+        nb = len(blocks)
+        stride = max(16, max(len(b) for b in blocks))
+        buf = np.zeros(nb * stride, dtype=np.uint8)
+        for j, b in enumerate(blocks):
+            buf[j * stride: j * stride + len(b)] = np.frombuffer(b, dtype=np.uint8)
+        lens = np.array([len(b) for b in blocks], dtype=np.uint32)
+        ostride = self.block_size * 3 + 65536
+        out = np.zeros(nb * ostride, dtype=np.uint8)
+        bits = np.zeros(nb, dtype=np.uint64)
+        _check(lib().bz2mi_compress_blocks(self._h, buf.ctypes.data, stride, lens.ctypes.data, nb,
+                                           out.ctypes.data, ostride, bits.ctypes.data))
+        res = []
+        for j in range(nb):
+            nbytes = (int(bits[j]) + 7) // 8
+            res.append((out[j * ostride: j * ostride + nbytes].tobytes(), int(bits[j])))
+        return res
+
+    def compress_device(self, d_in_ptr: int, n: int, d_out_ptr: int, cap: int, stream: int = 0) -> int:
+        """Device-resident whole stream; returns the compressed size."""
+        out_len = ctypes.c_size_t(0)
+        _check(lib().bz2mi_compress_device(self._h, d_in_ptr, n, d_out_ptr, cap, ctypes.byref(out_len),
+                                           stream or None))
+        return out_len.value
+
+    def timings(self):
+        arr = (ctypes.c_float * 6)()
+        _check(lib().bz2mi_last_timings(self._h, arr))
+        return dict(zip(("front", "bwt", "mtf", "seed", "huffman", "assemble"), list(arr)))
+
+
+def compress(data, level: int = 9, parallel: int = 10, unit: int = 10000, device: int = 0) -> bytes:
+    with Context(level, parallel, unit, device) as ctx:
+        return ctx.compress(data)
+
+
+class OutputStream:
+    """Python mirror of the reference OutputStream (OutputStream.hpp:35-241):
+    bytes written through write() come out as a .bz2 stream on close()."""
+
+    def __init__(self, out, block_size_multiplier: int = 9, parallel_block_cnt: int = 10, unit: int = 10000):
+        if block_size_multiplier < 1 or block_size_multiplier > 9:
+            raise ValueError("Invalid block size")
+        if parallel_block_cnt < 1:
+            raise ValueError("Invalid parallel block count")
+        self._out = out
+        self._buf = bytearray()
+        self._finished = False
+        self._ctx = Context(block_size_multiplier, parallel_block_cnt, unit)
+
+    def write(self, value, offset: int = 0, length: int | None = None) -> None:
+        if self._finished:
+            raise RuntimeError("Write beyond end of stream")
+        if isinstance(value, int):
+            self._buf.append(value & 0xFF)
+        else:
+            data = bytes(value)
+            if length is None:
+                length = len(data) - offset
+            self._buf += data[offset: offset + length]
+
+    def close(self) -> None:
+        if not self._finished:
+            self._finished = True
+            self._out.write(self._ctx.compress(bytes(self._buf)))
+            self._ctx.close()

@@ -1,0 +1,427 @@
+// C-ABI launcher of libbz2mi (include/bz2mi.h): device memory, the per-batch
+// kernel sequence and the stream state that OutputStream keeps in the
+// reference (OutputStream.hpp:35-61).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bz2mi.h"
+#include "common.hpp"
+#include "kernels.hpp"
+#include "rle1.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHECK(expr)                                                                        \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(BZ2MI_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+template <class T>
+int dalloc(T** p, size_t count) {
+    if (*p) {
+        (void)hipFree(*p);
+        *p = nullptr;
+    }
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return fail(BZ2MI_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    return BZ2MI_OK;
+}
+
+}  // namespace
+
+struct bz2mi_ctx {
+    int level = 9, p = 10, unit = 10000, S = 90000, device = 0;
+    size_t stride = 0;           // device bytes per block slot
+    size_t mtf_stride = 0;       // uint16 per block
+    size_t payload_words = 0;    // uint32 per block
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int cap = 0;                 // blocks the batch buffers hold
+    int bwt_slots = 0;
+
+    uint8_t* d_blocks = nullptr;
+    uint32_t* d_lens = nullptr;
+    uint32_t* d_crc = nullptr;
+    uint8_t* d_bwt = nullptr;
+    uint32_t* d_orig = nullptr;
+    uint8_t* d_ranks = nullptr;
+    uint8_t* d_rec = nullptr;
+    uint16_t* d_mtf = nullptr;
+    uint32_t* d_mtflen = nullptr;
+    uint32_t* d_alpha = nullptr;
+    uint32_t* d_hist = nullptr;
+    uint32_t* d_present = nullptr;
+    uint32_t* d_seed = nullptr;
+    uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
+    uint32_t* d_payload = nullptr;
+    uint64_t* d_pbits = nullptr;
+    uint64_t* d_offs = nullptr;
+    uint32_t* d_out = nullptr;
+    size_t out_words = 0;
+    uint8_t* d_scratch = nullptr;
+    uint32_t* d_counter = nullptr;
+    hipEvent_t ev[8] = {};
+    float last_ms[6] = {0, 0, 0, 0, 0, 0};
+
+    // stream state (OutputStream.hpp:39-44)
+    uint64_t blocks_done = 0;
+    uint32_t stream_crc = 0;
+    uint64_t carry = 0;      // MSB-aligned pending bits
+    int carry_bits = 0;
+    bool header_done = false;
+    bool finished = false;
+
+    std::vector<uint8_t> h_stage;
+};
+
+namespace {
+
+// BZ2MI_SYNC_DEBUG=1: synchronise and report after every launch (debug aid).
+bool sync_debug() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("BZ2MI_SYNC_DEBUG");
+        v = (e && *e && *e != '0') ? 1 : 0;
+    }
+    return v == 1;
+}
+
+#define STAGE_DONE(name)                                                              \
+    do {                                                                              \
+        if (sync_debug()) {                                                           \
+            hipError_t e2_ = hipStreamSynchronize(s);                                 \
+            fprintf(stderr, "[bz2mi] %s done: %s\n", name, hipGetErrorString(e2_));   \
+        }                                                                             \
+    } while (0)
+
+int ensure_capacity(bz2mi_ctx* c, int nblocks) {
+    if (nblocks <= c->cap) return BZ2MI_OK;
+    int cap = std::max(nblocks, 16);
+    const size_t B = (size_t)cap;
+    int r;
+    if ((r = dalloc(&c->d_blocks, B * c->stride))) return r;
+    if ((r = dalloc(&c->d_lens, B))) return r;
+    if ((r = dalloc(&c->d_crc, B))) return r;
+    if ((r = dalloc(&c->d_bwt, B * c->stride))) return r;
+    if ((r = dalloc(&c->d_orig, B))) return r;
+    if ((r = dalloc(&c->d_ranks, B * c->stride))) return r;
+    if ((r = dalloc(&c->d_rec, B * 64 * 256))) return r;
+    if ((r = dalloc(&c->d_mtf, B * c->mtf_stride))) return r;
+    if ((r = dalloc(&c->d_mtflen, B))) return r;
+    if ((r = dalloc(&c->d_alpha, B))) return r;
+    if ((r = dalloc(&c->d_hist, B * bz2mi::kMaxAlpha))) return r;
+    if ((r = dalloc(&c->d_present, B * 8))) return r;
+    if ((r = dalloc(&c->d_seed, B * bz2mi::kMaxAlpha))) return r;
+    if ((r = dalloc(&c->d_payload, B * c->payload_words))) return r;
+    if ((r = dalloc(&c->d_pbits, B))) return r;
+    if ((r = dalloc(&c->d_offs, B + 1))) return r;
+    c->out_words = B * (c->payload_words + 4) + 64;
+    if ((r = dalloc(&c->d_out, c->out_words))) return r;
+    c->cap = cap;
+    return BZ2MI_OK;
+}
+
+// Kernel sequence for `nb` RLE1 blocks already in d_blocks/d_lens/d_crc.
+// Produces d_payload/d_pbits (and, with assemble, d_out).
+int run_blocks(bz2mi_ctx* c, int nb) {
+    using namespace bz2mi;
+    hipStream_t s = c->stream;
+    (void)hipGetLastError();
+    HIPCHECK(hipEventRecord(c->ev[0], s));
+    HIPCHECK(hipMemsetAsync(c->d_counter, 0, sizeof(uint32_t), s));
+    const int grid_bwt = std::min(nb, c->bwt_slots);
+    hipLaunchKernelGGL(bwt_kernel, dim3(grid_bwt), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens, nb,
+                       c->d_bwt, c->d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, c->d_counter);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("bwt");
+    HIPCHECK(hipEventRecord(c->ev[1], s));
+    hipLaunchKernelGGL(mtf_kernel, dim3(nb), dim3(64), 0, s, c->d_bwt, c->stride, c->d_lens, nb, c->d_ranks,
+                       c->d_rec, c->d_mtf, c->mtf_stride, c->d_mtflen, c->d_alpha, c->d_hist, c->d_present);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("mtf");
+    HIPCHECK(hipEventRecord(c->ev[2], s));
+    const int ne = c->p * kMaxAlpha;
+    hipLaunchKernelGGL(seed_kernel, dim3((ne + 255) / 256), dim3(256), 0, s, c->d_hist, c->d_seed, c->d_state, nb,
+                       c->p, (uint64_t)c->blocks_done);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("seed");
+    HIPCHECK(hipEventRecord(c->ev[3], s));
+    hipLaunchKernelGGL(huffman_kernel, dim3(nb), dim3(256), 0, s, c->d_mtf, c->mtf_stride, c->d_mtflen, c->d_alpha,
+                       c->d_seed, c->d_present, c->d_orig, nb, c->d_payload, c->payload_words, c->d_pbits);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("huffman");
+    HIPCHECK(hipEventRecord(c->ev[4], s));
+    return BZ2MI_OK;
+}
+
+int assemble(bz2mi_ctx* c, int nb, bool final_, uint8_t* out, size_t cap, size_t* out_len) {
+    using namespace bz2mi;
+    hipStream_t s = c->stream;
+    uint64_t prefix = c->carry;
+    int prefix_bits = c->carry_bits;
+    if (!c->header_done) {
+        // 'B' 'Z' 'h' '0'+level (OutputStream.hpp:126-128); nothing is carried yet
+        prefix = ((uint64_t)0x425a68u << 40) | ((uint64_t)('0' + c->level) << 32);
+        prefix_bits = 32;
+    }
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(256), 0, s, c->d_pbits, nb, (uint64_t)prefix_bits, c->d_offs);
+    HIPCHECK(hipGetLastError());
+    uint64_t end_bits = 0;
+    HIPCHECK(hipMemcpyAsync(&end_bits, c->d_offs + nb, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if (final_) end_bits += 80;
+    const uint64_t words = (end_bits + 31) / 32;
+    if (words > c->out_words) return fail(BZ2MI_ESPACE, "device output buffer too small");
+    hipLaunchKernelGGL(assemble_kernel, dim3(nb + 2), dim3(256), 0, s, c->d_payload, c->payload_words, c->d_offs,
+                       c->d_crc, nb, prefix, prefix_bits, final_ ? 1 : 0, c->stream_crc, c->d_out);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("assemble");
+    HIPCHECK(hipEventRecord(c->ev[5], s));
+    uint64_t total_bits = end_bits;
+    if (final_) total_bits = (total_bits + 7) & ~7ull;  // zero padding
+    const size_t nbytes = (size_t)(total_bits >> 3);
+    const int rem = (int)(total_bits & 7);
+    if (nbytes > cap) return fail(BZ2MI_ESPACE, "output buffer too small");
+    c->h_stage.resize(nbytes + 8);
+    HIPCHECK(hipMemcpyAsync(c->h_stage.data(), c->d_out, nbytes + (rem ? 1 : 0), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    std::memcpy(out, c->h_stage.data(), nbytes);
+    *out_len = nbytes;
+    c->carry = rem ? ((uint64_t)c->h_stage[nbytes] << 56) & (~0ull << (64 - rem)) : 0;
+    c->carry_bits = rem;
+    c->header_done = true;
+    if (nb > 0) {
+        float ms;
+        for (int i = 0; i < 5; ++i)
+            if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) c->last_ms[i + 1] = ms;
+    }
+    (void)hipGetLastError();  // timing queries must not leave a sticky error behind
+    return BZ2MI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* bz2mi_last_error(void) { return g_err.c_str(); }
+
+const char* bz2mi_version(void) { return "bz2mi 0.1 (gfx950)"; }
+
+int bz2mi_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+size_t bz2mi_compress_bound(size_t n, int level, int unit) {
+    const size_t S = (size_t)unit * (size_t)level;
+    const size_t blocks = (n + n / 4) / (S - 5) + 2;
+    const size_t per = (S + 1) * 20 / 8 + (S / 50 + 2) + 6 * 258 * 5 + 1024;
+    return 64 + blocks * per;
+}
+
+bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
+    if (level < 1 || level > 9) {
+        fail(BZ2MI_EINVAL, "Invalid block size");
+        return nullptr;
+    }
+    if (parallel_blocks < 1) {
+        fail(BZ2MI_EINVAL, "Invalid parallel block count");
+        return nullptr;
+    }
+    if (unit < 100 || (size_t)unit * level > (1u << 20) - 16) {
+        fail(BZ2MI_EINVAL, "Invalid block unit");
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+        fail(BZ2MI_EDEVICE, "no HIP device available for bz2mi");
+        return nullptr;
+    }
+    auto* c = new bz2mi_ctx();
+    c->level = level;
+    c->p = parallel_blocks;
+    c->unit = unit;
+    c->S = unit * level;
+    c->device = device;
+    c->stride = ((size_t)c->S + 16 + 63) & ~(size_t)63;
+    c->mtf_stride = ((size_t)c->S + 2 + 31) & ~(size_t)31;
+    {
+        const size_t S = (size_t)c->S;
+        const size_t bits = 24 + 272 + 18 + (S / 50 + 1) * 6 + 6 * (5 + 258 * 39) + (S + 1) * 20;
+        c->payload_words = (bits + 31) / 32 + 4;
+    }
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        fail(BZ2MI_EDEVICE, "hipStreamCreate failed");
+        delete c;
+        return nullptr;
+    }
+    c->own_stream = true;
+    hipDeviceProp_t prop;
+    int cus = 256;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+    c->bwt_slots = cus * 4;
+    if (dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S)) || dalloc(&c->d_counter, 4) ||
+        dalloc(&c->d_state, (size_t)c->p * bz2mi::kMaxAlpha)) {
+        bz2mi_destroy(c);
+        return nullptr;
+    }
+    (void)hipMemset(c->d_state, 0, sizeof(uint32_t) * c->p * bz2mi::kMaxAlpha);
+    for (auto& e : c->ev) (void)hipEventCreate(&e);
+    return c;
+}
+
+void bz2mi_destroy(bz2mi_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void* ptrs[] = {c->d_blocks, c->d_lens, c->d_crc, c->d_bwt, c->d_orig, c->d_ranks, c->d_rec, c->d_mtf,
+                    c->d_mtflen, c->d_alpha, c->d_hist, c->d_present, c->d_seed, c->d_state, c->d_payload,
+                    c->d_pbits, c->d_offs, c->d_out, c->d_scratch, c->d_counter};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+uint64_t bz2mi_blocks_done(const bz2mi_ctx* c) { return c ? c->blocks_done : 0; }
+
+int bz2mi_last_timings(bz2mi_ctx* c, float* ms6) {
+    if (!c || !ms6) return fail(BZ2MI_EINVAL, "null argument");
+    for (int i = 0; i < 6; ++i) ms6[i] = c->last_ms[i];
+    return BZ2MI_OK;
+}
+
+int bz2mi_compress_blocks(bz2mi_ctx* c, const uint8_t* blocks, size_t stride, const uint32_t* lens,
+                          uint32_t nblocks, uint8_t* out, size_t out_stride, uint64_t* out_bits) {
+    if (!c || (!blocks && nblocks) || !lens) return fail(BZ2MI_EINVAL, "null argument");
+    if (c->finished) return fail(BZ2MI_ESTATE, "Write beyond end of stream");
+    if (nblocks == 0) return BZ2MI_OK;
+    for (uint32_t j = 0; j < nblocks; ++j)
+        if (lens[j] < 1 || lens[j] > (uint32_t)c->S) return fail(BZ2MI_EINVAL, "block length out of range");
+    HIPCHECK(hipSetDevice(c->device));
+    int r;
+    if ((r = ensure_capacity(c, (int)nblocks))) return r;
+    HIPCHECK(hipMemcpy2DAsync(c->d_blocks, c->stride, blocks, stride, std::min(stride, c->stride), nblocks,
+                              hipMemcpyHostToDevice, c->stream));
+    HIPCHECK(hipMemcpyAsync(c->d_lens, lens, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    if ((r = run_blocks(c, (int)nblocks))) return r;
+    std::vector<uint64_t> bits(nblocks);
+    HIPCHECK(hipMemcpyAsync(bits.data(), c->d_pbits, nblocks * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (uint32_t j = 0; j < nblocks; ++j) {
+        const size_t nbytes = (size_t)((bits[j] + 7) / 8);
+        if (nbytes > out_stride) return fail(BZ2MI_ESPACE, "out_stride too small");
+        HIPCHECK(hipMemcpy(out + (size_t)j * out_stride, c->d_payload + (size_t)j * c->payload_words, nbytes,
+                           hipMemcpyDeviceToHost));
+        out_bits[j] = bits[j];
+    }
+    c->blocks_done += nblocks;
+    return BZ2MI_OK;
+}
+
+int bz2mi_compress_rle1(bz2mi_ctx* c, const uint8_t* blocks, size_t stride, const uint32_t* lens,
+                        const uint32_t* crcs, uint32_t nblocks, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!c || !out_len || (nblocks && (!blocks || !lens || !crcs))) return fail(BZ2MI_EINVAL, "null argument");
+    if (c->finished) return fail(BZ2MI_ESTATE, "Write beyond end of stream");
+    *out_len = 0;
+    if (nblocks == 0) return BZ2MI_OK;
+    for (uint32_t j = 0; j < nblocks; ++j)
+        if (lens[j] < 1 || lens[j] > (uint32_t)c->S) return fail(BZ2MI_EINVAL, "block length out of range");
+    HIPCHECK(hipSetDevice(c->device));
+    int r;
+    if ((r = ensure_capacity(c, (int)nblocks))) return r;
+    HIPCHECK(hipMemcpy2DAsync(c->d_blocks, c->stride, blocks, stride, std::min(stride, c->stride), nblocks,
+                              hipMemcpyHostToDevice, c->stream));
+    HIPCHECK(hipMemcpyAsync(c->d_lens, lens, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHECK(hipMemcpyAsync(c->d_crc, crcs, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    if ((r = run_blocks(c, (int)nblocks))) return r;
+    if ((r = assemble(c, (int)nblocks, false, out, cap, out_len))) return r;
+    for (uint32_t j = 0; j < nblocks; ++j) c->stream_crc = ((c->stream_crc << 1) | (c->stream_crc >> 31)) ^ crcs[j];
+    c->blocks_done += nblocks;
+    return BZ2MI_OK;
+}
+
+int bz2mi_finish(bz2mi_ctx* c, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!c || !out_len) return fail(BZ2MI_EINVAL, "null argument");
+    if (c->finished) {
+        *out_len = 0;
+        return BZ2MI_OK;
+    }
+    HIPCHECK(hipSetDevice(c->device));
+    int r;
+    if ((r = ensure_capacity(c, 1))) return r;
+    if ((r = assemble(c, 0, true, out, cap, out_len))) return r;
+    c->finished = true;
+    return BZ2MI_OK;
+}
+
+int bz2mi_compress(bz2mi_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!c || !out_len || (n && !in)) return fail(BZ2MI_EINVAL, "null argument");
+    if (c->finished || c->blocks_done || c->header_done) return fail(BZ2MI_ESTATE, "context already used");
+    // host RLE1 split into batches, device compression per batch
+    const int S = c->S;
+    const size_t hstride = c->stride;
+    const int batch = 4096;
+    std::vector<uint8_t> blocks((size_t)batch * hstride);
+    std::vector<uint32_t> lens(batch), crcs(batch);
+    size_t pos = 0, o = 0;
+    while (pos < n) {
+        int nb = 0;
+        while (nb < batch && pos < n) {
+            bz2mi::Rle1Block blk;
+            blk.begin(blocks.data() + (size_t)nb * hstride, S);
+            pos += blk.put_many(in + pos, n - pos);
+            blk.finish();
+            lens[nb] = (uint32_t)blk.len;
+            crcs[nb] = blk.block_crc();
+            nb++;
+        }
+        size_t got = 0;
+        int r = bz2mi_compress_rle1(c, blocks.data(), hstride, lens.data(), crcs.data(), (uint32_t)nb, out + o,
+                                    cap - o, &got);
+        if (r) return r;
+        o += got;
+    }
+    size_t got = 0;
+    int r = bz2mi_finish(c, out + o, cap - o, &got);
+    if (r) return r;
+    *out_len = o + got;
+    return BZ2MI_OK;
+}
+
+int bz2mi_compress_device(bz2mi_ctx* c, const void* d_in, size_t n, void* d_out, size_t cap, size_t* out_len,
+                          void* hip_stream) {
+    (void)c;
+    (void)d_in;
+    (void)n;
+    (void)d_out;
+    (void)cap;
+    (void)out_len;
+    (void)hip_stream;
+    return fail(BZ2MI_EINVAL, "bz2mi_compress_device: not built yet");
+}
+
+}  // extern "C"

@@ -1,0 +1,203 @@
+// Shared device helpers and constants for the bz2mi HIP kernels (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bz2mi {
+
+// Format constants (reference include/Config.hpp:27-47).
+constexpr int kBlockMagicHi = 0x314159;
+constexpr int kBlockMagicLo = 0x265359;
+constexpr int kEosMagicHi = 0x177245;
+constexpr int kEosMagicLo = 0x385090;
+constexpr int kGroupRun = 50;      // HUFFMAN_GROUP_RUN_LENGTH
+constexpr int kMaxAlpha = 258;     // HUFFMAN_MAXIMUM_ALPHABET_SIZE
+constexpr int kMaxTables = 6;      // HUFFMAN_MAXIMUM_TABLES
+constexpr int kMaxCodeLen = 20;    // HUFFMAN_ENCODE_MAXIMUM_CODE_LENGTH
+constexpr int kHighCost = 15;      // HUFFMAN_HIGH_SYMBOL_COST
+constexpr int kHeaderBits = 81;    // 48-bit block magic + 32-bit CRC + randomised bit
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ uint32_t uniform(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    const uint32_t lo = uniform((uint32_t)x), hi = uniform((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Inclusive scans over one 64-lane wave.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x = x > y ? x : y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+    return x;
+}
+
+// Exclusive sum over a workgroup of NT threads.  `tmp` needs NT/64 words of
+// LDS.  Returns the exclusive prefix; *total receives the workgroup sum.
+template <int NT>
+__device__ __forceinline__ uint32_t wg_excl_sum(uint32_t v, uint32_t* tmp, uint32_t* total) {
+    constexpr int NW = NT / 64;
+    const uint32_t inc = wave_incl_sum(v);
+    if (lane_id() == 63) tmp[wave_id()] = inc;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        uint32_t t = tmp[w];
+        base += (w < wave_id()) ? t : 0u;
+        all += t;
+    }
+    __syncthreads();
+    *total = uniform(all);
+    return base + inc - v;
+}
+
+template <int NT>
+__device__ __forceinline__ uint64_t wg_excl_sum64(uint64_t v, uint64_t* tmp, uint64_t* total) {
+    constexpr int NW = NT / 64;
+    const uint64_t inc = wave_incl_sum64(v);
+    if (lane_id() == 63) tmp[wave_id()] = inc;
+    __syncthreads();
+    uint64_t base = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        uint64_t t = tmp[w];
+        base += (w < wave_id()) ? t : 0ull;
+        all += t;
+    }
+    __syncthreads();
+    *total = uniform64(all);
+    return base + inc - v;
+}
+
+// Inclusive max over a workgroup (values are indices, so 0 is neutral).
+template <int NT>
+__device__ __forceinline__ uint32_t wg_incl_max(uint32_t v, uint32_t* tmp, uint32_t* total) {
+    constexpr int NW = NT / 64;
+    const uint32_t inc = wave_incl_max(v);
+    if (lane_id() == 63) tmp[wave_id()] = inc;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        uint32_t t = tmp[w];
+        if (w < wave_id()) base = base > t ? base : t;
+        all = all > t ? all : t;
+    }
+    __syncthreads();
+    *total = uniform(all);
+    return inc > base ? inc : base;
+}
+
+// Mask of the lanes of this wave whose `key` (8 bits) equals this lane's,
+// restricted to `valid` lanes.
+__device__ __forceinline__ uint64_t wave_match8(uint32_t key, bool valid) {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (key >> b) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+    }
+    return peers;
+}
+
+// Write `count` (1..32) bits of `value`, MSB-first, at absolute bit `pos` of
+// a big-endian bit stream held in 32-bit words (byte-swapped on store so the
+// memory image is the byte stream).  Used for words shared between writers.
+__device__ __forceinline__ void put_bits_or(uint32_t* out, uint64_t pos, int count, uint32_t value) {
+    const uint64_t w = pos >> 5;
+    const int off = (int)(pos & 31);
+    const uint64_t v = ((uint64_t)(value & (count == 32 ? 0xffffffffu : ((1u << count) - 1u))))
+                       << (64 - count - off);
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    if (hi) atomicOr(&out[w], bswap32(hi));
+    if (lo) atomicOr(&out[w + 1], bswap32(lo));
+}
+
+// Sequential bit writer owned by one thread over [start, end): interior words
+// are plain stores, the first and last (possibly shared) words use atomicOr.
+// The destination words must be zero beforehand.
+struct BitSink {
+    uint32_t* out;
+    uint64_t start;   // first bit this writer owns
+    uint64_t pos;     // next bit position
+    uint64_t acc;     // pending bits, MSB-aligned
+    int nacc;
+
+    __device__ void init(uint32_t* o, uint64_t p) {
+        out = o;
+        start = p;
+        pos = p;
+        acc = 0;
+        nacc = (int)(p & 31);  // leading bits of the first word are someone else's
+    }
+    __device__ __forceinline__ void flush_word(bool last) {
+        const uint64_t w = (pos - (uint64_t)nacc) >> 5;
+        const uint32_t word = (uint32_t)(acc >> 32);
+        const bool shared = (w << 5) < start || last;
+        if (shared) {
+            if (word) atomicOr(&out[w], bswap32(word));
+        } else {
+            out[w] = bswap32(word);
+        }
+    }
+    __device__ __forceinline__ void put(int count, uint32_t value) {
+        // count <= 32
+        const uint64_t v = (uint64_t)(value & (count == 32 ? 0xffffffffu : ((1u << count) - 1u)));
+        acc |= (v << (64 - count)) >> nacc;
+        nacc += count;
+        pos += count;
+        if (nacc >= 32) {
+            flush_word(false);
+            acc <<= 32;
+            nacc -= 32;
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if (nacc > 0) {
+            // partially filled last word: shared with the next writer
+            const uint64_t w = (pos - (uint64_t)nacc) >> 5;
+            const uint32_t word = (uint32_t)(acc >> 32);
+            if (word) atomicOr(&out[w], bswap32(word));
+        }
+    }
+};
+
+}  // namespace bz2mi

@@ -1,0 +1,35 @@
+// Kernel entry points of libbz2mi (declarations shared by the .hip files and
+// the host launcher in api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bz2mi {
+
+// Scratch bytes one BWT workgroup slot needs for blocks of S bytes.
+inline size_t bwt_slot_bytes(int S) { return (size_t)40 * (size_t)S + 256; }
+
+__global__ void bwt_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
+                           uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,
+                           int S, uint32_t* work_counter);
+
+__global__ void mtf_kernel(const uint8_t* bwt, size_t stride, const uint32_t* lens, int nblocks, uint8_t* ranks,
+                           uint8_t* rec, uint16_t* mtf_out, size_t mtf_stride, uint32_t* mtf_len,
+                           uint32_t* alpha_out, uint32_t* hist_out, uint32_t* present_out);
+
+__global__ void seed_kernel(const uint32_t* hist, uint32_t* seed, uint32_t* state, int nblocks, int p,
+                            uint64_t first_block);
+
+__global__ void huffman_kernel(const uint16_t* mtf, size_t mtf_stride, const uint32_t* mtf_len,
+                               const uint32_t* alpha_in, const uint32_t* seed, const uint32_t* present,
+                               const uint32_t* orig, int nblocks, uint32_t* payload, size_t payload_words,
+                               uint64_t* payload_bits);
+
+__global__ void offsets_kernel(const uint64_t* bits, int nblocks, uint64_t prefix_bits, uint64_t* offs);
+
+__global__ void assemble_kernel(const uint32_t* payload, size_t payload_words, const uint64_t* offs,
+                                const uint32_t* crc, int nblocks, uint64_t prefix, int prefix_bits, int final_,
+                                uint32_t stream_crc, uint32_t* out);
+
+}  // namespace bz2mi

@@ -1,0 +1,271 @@
+// Move-to-front + RLE2 (zero-run RUNA/RUNB coding) on the device.
+//
+// Restates MTFAndRLE2StageEncoder / valueToFront (reference
+// kernel.cpp:2514-2533, 2561-2649) with exact sequential semantics, but
+// chunk-parallel: one 64-lane wave per block, lane c owns chunk c.
+//   1. recency pass: lane c scans its chunk backwards and records the distinct
+//      bytes in order of last occurrence (the front of any MTF list after the
+//      chunk), plus the chunk's byte set.
+//   2. list build: the MTF list at the start of chunk c is the recency lists of
+//      chunks c-1, c-2, ... merged (first occurrence wins), followed by the
+//      block's remaining symbols in ascending order -- the reference's identity
+//      initial list restricted to the symbols in use (symbol map, :2565-2572).
+//   3. MTF pass: lane-serial move-to-front over a byte list in LDS, fused
+//      search-and-shift on 32-bit words; ranks go to a byte scratch array and
+//      the lane records its zero-run boundary state and histogram.
+//   4. a wave scan assigns every zero run to the lane where it starts and
+//      computes each lane's output offset; lanes then emit RUNA/RUNB digits
+//      (bijective base 2, :2585-2606) and rank+1 symbols, and lane 63 the EOB.
+// The per-block histogram of the emitted symbols (258 bins) is what the
+// reference adds into its persistent frequency array (:2613, :2641-2643).
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace bz2mi {
+
+namespace {
+
+constexpr int NL = 64;
+
+struct MtfShared {
+    uint32_t lists[NL][64];   // per-lane MTF list, 256 bytes as 64 little-endian words
+    uint32_t mask[NL][8];     // per-lane byte set
+    uint32_t present[8];
+    uint32_t hist[kMaxAlpha];
+};
+
+__device__ __forceinline__ void run_digits(uint32_t r, uint32_t& a, uint32_t& b, uint32_t& nd) {
+    uint32_t rep = r - 1;
+    for (;;) {
+        if ((rep & 1u) == 0) a++;
+        else b++;
+        nd++;
+        if (rep <= 1) break;
+        rep = (rep - 2) >> 1;
+    }
+}
+
+__device__ __forceinline__ void emit_run(uint32_t r, uint16_t* out, uint32_t& o) {
+    uint32_t rep = r - 1;
+    for (;;) {
+        out[o++] = (uint16_t)(rep & 1u);  // RUNA = 0, RUNB = 1
+        if (rep <= 1) break;
+        rep = (rep - 2) >> 1;
+    }
+}
+
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt, size_t stride,
+                                                 const uint32_t* __restrict__ lens, int nblocks,
+                                                 uint8_t* __restrict__ ranks, uint8_t* __restrict__ rec,
+                                                 uint16_t* __restrict__ mtf_out, size_t mtf_stride,
+                                                 uint32_t* __restrict__ mtf_len, uint32_t* __restrict__ alpha_out,
+                                                 uint32_t* __restrict__ hist_out,
+                                                 uint32_t* __restrict__ present_out) {
+    __shared__ MtfShared sh;
+    const int b = blockIdx.x;
+    if (b >= nblocks) return;
+    const int c = threadIdx.x;  // lane == chunk
+    const int n = (int)lens[b];
+    const uint8_t* X = bwt + (size_t)b * stride;
+    uint8_t* R = ranks + (size_t)b * stride;
+    uint8_t* myrec = rec + ((size_t)b * NL + c) * 256;
+    uint16_t* out = mtf_out + (size_t)b * mtf_stride;
+
+    int L = (n + NL - 1) / NL;
+    L = (L + 3) & ~3;
+    const int c0 = min(c * L, n);
+    const int c1 = min(c0 + L, n);
+
+    // ---- 1. recency lists (backwards scan)
+    for (int q = 0; q < 8; ++q) sh.mask[c][q] = 0;
+    for (int s = c; s < kMaxAlpha; s += NL) sh.hist[s] = 0;
+    int rcnt = 0;
+    for (int i = c1 - 1; i >= c0; --i) {
+        const uint32_t v = X[i];
+        const uint32_t bit = 1u << (v & 31);
+        uint32_t m = sh.mask[c][v >> 5];
+        if (!(m & bit)) {
+            sh.mask[c][v >> 5] = m | bit;
+            myrec[rcnt++] = (uint8_t)v;
+        }
+    }
+    __syncthreads();
+    if (c < 8) {
+        uint32_t p = 0;
+        for (int l = 0; l < NL; ++l) p |= sh.mask[l][c];
+        sh.present[c] = p;
+    }
+    // recency counts are the popcounts of the lane masks
+    __syncthreads();
+    int k = 0;
+    for (int q = 0; q < 8; ++q) k += __popc(sh.present[q]);
+
+    // ---- 2. initial list of chunk c
+    uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t* Lw = sh.lists[c];
+    int len = 0;
+    uint32_t word = 0;
+    auto push = [&](uint32_t v) {
+        word |= v << ((len & 3) * 8);
+        if ((len & 3) == 3) {
+            Lw[len >> 2] = word;
+            word = 0;
+        }
+        len++;
+    };
+    for (int cc = c - 1; cc >= 0 && len < k; --cc) {
+        const uint8_t* r = rec + ((size_t)b * NL + cc) * 256;
+        int cnt = 0;
+        for (int q = 0; q < 8; ++q) cnt += __popc(sh.mask[cc][q]);
+        for (int j = 0; j < cnt; ++j) {
+            const uint32_t v = r[j];
+            const uint32_t bit = 1u << (v & 31);
+            bool had = false;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q == (int)(v >> 5)) {
+                    had = (seen[q] & bit) != 0;
+                    seen[q] |= bit;
+                }
+            if (!had) push(v);
+        }
+    }
+    for (int q = 0; q < 8; ++q) {
+        uint32_t rest = sh.present[q] & ~seen[q];
+        while (rest) {
+            const int z = __ffs(rest) - 1;
+            rest &= rest - 1;
+            push((uint32_t)(q * 32 + z));
+        }
+    }
+    if (len & 3) Lw[len >> 2] = word;
+
+    // ---- 3. MTF pass
+    uint32_t zl = 0, zt = 0, nz = 0, run = 0, idig = 0, ia = 0, ib = 0;
+    bool seen_nz = false;
+    uint32_t pack = 0;
+    for (int i = c0; i < c1; ++i) {
+        const uint32_t v = X[i];
+        const uint32_t vv = v * 0x01010101u;
+        uint32_t carry = v;
+        int pos = 0;
+        for (int j = 0; j < 64; ++j) {  // bounded: v is always in the list
+            const uint32_t w = Lw[j];
+            const uint32_t x = w ^ vv;
+            const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
+            const uint32_t sh8 = (w << 8) | carry;
+            if (z) {
+                const int byte = __ffs(z) / 8 - 1;  // first matching byte
+                const uint32_t low = byte == 3 ? 0xffffffffu : ((1u << ((byte + 1) * 8)) - 1u);
+                Lw[j] = (w & ~low) | (sh8 & low);
+                pos = j * 4 + byte;
+                break;
+            }
+            Lw[j] = sh8;
+            carry = w >> 24;
+        }
+        pack |= (uint32_t)pos << ((i & 3) * 8);
+        if ((i & 3) == 3) *(uint32_t*)(R + (i & ~3)) = pack, pack = 0;
+        if (pos == 0) {
+            run++;
+        } else {
+            if (run > 0) {
+                if (seen_nz) run_digits(run, ia, ib, idig);
+                else zl = run;
+                run = 0;
+            }
+            seen_nz = true;
+            nz++;
+            atomicAdd(&sh.hist[pos + 1], 1u);
+        }
+    }
+    if (c1 > c0 && (c1 & 3)) *(uint32_t*)(R + (c1 & ~3)) = pack;
+    if (run > 0) {
+        zt = run;
+        if (!seen_nz) zl = run;
+    }
+    // ---- 4. zero-run ownership and offsets
+    const int clen = c1 - c0;
+    const uint32_t firstnz = seen_nz ? (uint32_t)(c0 + zl) : (uint32_t)n;
+    // next nonzero strictly after this chunk: suffix min over lanes c+1..
+    uint32_t nxt = firstnz;
+    for (int d = 1; d < NL; d <<= 1) {
+        uint32_t y = __shfl_down(nxt, d);
+        if (c + d < NL) nxt = nxt < y ? nxt : y;
+    }
+    uint32_t after = __shfl_down(nxt, 1);
+    if (c == NL - 1) after = (uint32_t)n;
+    const uint32_t prev_zt = __shfl_up(zt, 1);
+    const bool prev_ends_zero = c > 0 && prev_zt > 0;
+    uint32_t bdig = 0, ba = 0, bb = 0;
+    uint32_t lead_len = 0, tail_len = 0;
+    bool own_lead = false;
+    if (clen > 0) {
+        if (!seen_nz) {
+            if (!prev_ends_zero) {  // an all-zero chunk that starts a run
+                own_lead = true;
+                lead_len = after - (uint32_t)c0;
+                run_digits(lead_len, ba, bb, bdig);
+            }
+        } else {
+            if (zl > 0 && !prev_ends_zero) {
+                own_lead = true;
+                lead_len = zl;
+                run_digits(lead_len, ba, bb, bdig);
+            }
+            if (zt > 0) {
+                tail_len = after - (uint32_t)(c1 - zt);
+                run_digits(tail_len, ba, bb, bdig);
+            }
+        }
+    }
+    const uint32_t cnt = nz + idig + bdig;
+    const uint32_t incl = wave_incl_sum(cnt);
+    const uint32_t off = incl - cnt;
+    const uint32_t total = __shfl(incl, NL - 1);
+    const uint32_t runA = wave_sum(ia + ba), runB = wave_sum(ib + bb);
+
+    // ---- 5. emission
+    uint32_t o = off;
+    if (clen > 0) {
+        run = 0;
+        int i = c0;
+        if (!own_lead && (zl > 0 || !seen_nz)) i = c0 + (int)zl;  // tail of an earlier lane's run
+        bool lead = own_lead;
+        for (; i < c1; ++i) {
+            const uint32_t r = R[i];
+            if (r == 0) {
+                run++;
+            } else {
+                if (run > 0) {
+                    emit_run(lead ? lead_len : run, out, o);
+                    run = 0;
+                }
+                lead = false;
+                out[o++] = (uint16_t)(r + 1);
+            }
+        }
+        if (run > 0) emit_run(lead ? lead_len : tail_len, out, o);
+    }
+    __syncthreads();
+    const uint32_t eob = (uint32_t)k + 1;
+    if (c == NL - 1) {
+        out[total] = (uint16_t)eob;
+        mtf_len[b] = total + 1;
+        alpha_out[b] = eob + 1;
+    }
+    uint32_t* H = hist_out + (size_t)b * kMaxAlpha;
+    for (int s = c; s < kMaxAlpha; s += NL) {
+        uint32_t h = sh.hist[s];
+        if (s == 0) h += runA;
+        if (s == 1) h += runB;
+        if ((uint32_t)s == eob) h += 1;
+        H[s] = h;
+    }
+    if (c < 8) present_out[(size_t)b * 8 + c] = sh.present[c];
+}
+
+}  // namespace bz2mi

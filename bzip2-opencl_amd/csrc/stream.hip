@@ -1,0 +1,169 @@
+// Cross-block kernels: the per-slot seed carry-over and the bit-level stream
+// assembly.
+//
+// seed_kernel restates the reference's never-cleared per-slot MTF frequency
+// array (OutputStream.hpp:93 allocated once, kernel.cpp:2613/2641-2643 adding
+// into it, kernel.cpp:2859-2893 reading it): block b of the stream seeds its
+// Huffman tables from the running sum of the histograms of every earlier block
+// that used the same slot (b mod p), itself included.
+//
+// offsets_kernel / assemble_kernel replace the host bit stitching of
+// OutputStream::closeBlocks (OutputStream.hpp:192-239) and
+// BitOutputStream.hpp:30-99: blocks are concatenated at bit granularity, each
+// as 81 header bits (0x314159265359, block CRC, randomised=0) followed by its
+// payload; an optional prefix (stream header and/or carried bits) and the
+// end-of-stream trailer (0x177245385090, stream CRC, zero pad) frame them.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace bz2mi {
+
+__global__ void seed_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ seed,
+                            uint32_t* __restrict__ state, int nblocks, int p, uint64_t first_block) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= p * kMaxAlpha) return;
+    const int slot = e / kMaxAlpha, sym = e % kMaxAlpha;
+    // first batch-local block that maps to `slot`
+    const int r = (int)(first_block % (uint64_t)p);
+    int b = slot - r;
+    if (b < 0) b += p;
+    uint32_t acc = state[e];
+    for (; b < nblocks; b += p) {
+        acc += hist[(size_t)b * kMaxAlpha + sym];
+        seed[(size_t)b * kMaxAlpha + sym] = acc;
+    }
+    state[e] = acc;
+}
+
+// offs[b] = prefix_bits + sum_{b'<b} (81 + bits[b']); offs[nblocks] = end.
+__global__ __launch_bounds__(256) void offsets_kernel(const uint64_t* __restrict__ bits, int nblocks,
+                                                      uint64_t prefix_bits, uint64_t* __restrict__ offs) {
+    __shared__ uint64_t tmp[4];
+    uint64_t carry = prefix_bits;
+    for (int base = 0; base < nblocks; base += 256) {
+        const int b = base + threadIdx.x;
+        const uint64_t v = b < nblocks ? bits[b] + (uint64_t)kHeaderBits : 0;
+        uint64_t tot;
+        const uint64_t ex = wg_excl_sum64<256>(v, tmp, &tot);
+        if (b < nblocks) offs[b] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) offs[nblocks] = carry;
+}
+
+namespace {
+
+struct Frame {
+    const uint32_t* payload;
+    size_t payload_words;
+    const uint64_t* offs;
+    const uint32_t* crc;
+    int nblocks;
+    uint64_t prefix;       // MSB-aligned prefix bits
+    int prefix_bits;
+    int final_;
+    uint32_t stream_crc;
+};
+
+// Up to `want` (<=32) bits starting at absolute position `pos`, taken from the
+// segment `seg` (-1 prefix, 0..nblocks-1 blocks, nblocks trailer) that holds
+// `pos`; returns the number of bits taken (stops at the segment's end).
+__device__ int seg_bits(const Frame& f, int seg, uint64_t pos, int want, uint32_t* out) {
+    uint64_t s0, s1;
+    if (seg < 0) {
+        s0 = 0;
+        s1 = (uint64_t)f.prefix_bits;
+    } else if (seg < f.nblocks) {
+        s0 = f.offs[seg];
+        s1 = f.offs[seg + 1];
+    } else {
+        s0 = f.offs[f.nblocks];
+        s1 = s0 + (f.final_ ? 80u : 0u);
+    }
+    const uint64_t local = pos - s0;
+    int take = (int)((s1 - pos) < (uint64_t)want ? (s1 - pos) : (uint64_t)want);
+    if (take <= 0) {
+        *out = 0;
+        return 0;
+    }
+    uint64_t win;  // 64-bit MSB-first window starting at `local`
+    if (seg < 0) {
+        win = f.prefix << local;
+    } else if (seg == f.nblocks) {
+        const uint32_t c = f.stream_crc;
+        const uint32_t w[3] = {0x17724538u, 0x50900000u | (c >> 16), c << 16};
+        const int wi = (int)(local >> 5), sh = (int)(local & 31);
+        const uint64_t hi = ((uint64_t)w[wi] << 32) | (wi + 1 < 3 ? w[wi + 1] : 0u);
+        win = hi << sh;
+    } else if (local < (uint64_t)kHeaderBits) {
+        const uint32_t c = f.crc[seg];
+        const uint32_t w[3] = {0x31415926u, 0x53590000u | (c >> 16), c << 16};
+        const int wi = (int)(local >> 5), sh = (int)(local & 31);
+        const uint64_t hi = ((uint64_t)w[wi] << 32) | (wi + 1 < 3 ? w[wi + 1] : 0u);
+        win = hi << sh;
+        const int left = kHeaderBits - (int)local;
+        take = take < left ? take : left;
+    } else {
+        const uint64_t q = local - kHeaderBits;
+        const uint32_t* W = f.payload + (size_t)seg * f.payload_words;
+        const size_t wi = q >> 5;
+        const int sh = (int)(q & 31);
+        const uint64_t hi = ((uint64_t)bswap32(W[wi]) << 32) | bswap32(W[wi + 1]);
+        win = hi << sh;
+    }
+    *out = (uint32_t)(win >> 32) >> (32 - take) << (32 - take);  // top `take` bits, MSB-aligned
+    return take;
+}
+
+}  // namespace
+
+// One workgroup per block (plus the prefix in workgroup 0): every output word
+// is built by the segment that holds its first bit, so no word is written
+// twice and no atomics are needed.
+__global__ __launch_bounds__(256) void assemble_kernel(const uint32_t* __restrict__ payload, size_t payload_words,
+                                                       const uint64_t* __restrict__ offs,
+                                                       const uint32_t* __restrict__ crc, int nblocks,
+                                                       uint64_t prefix, int prefix_bits, int final_,
+                                                       uint32_t stream_crc, uint32_t* __restrict__ out) {
+    Frame f{payload, payload_words, offs, crc, nblocks, prefix, prefix_bits, final_, stream_crc};
+    const uint64_t end = offs[nblocks] + (final_ ? 80u : 0u);
+    // segment handled by this workgroup: blockIdx.x - 1 (workgroup 0: prefix)
+    const int seg0 = (int)blockIdx.x - 1;
+    if (seg0 > nblocks) return;
+    uint64_t lo, hi;
+    if (seg0 < 0) {
+        lo = 0;
+        hi = (uint64_t)prefix_bits;
+    } else if (seg0 < nblocks) {
+        lo = offs[seg0];
+        hi = offs[seg0 + 1];
+    } else {
+        lo = offs[nblocks];
+        hi = end;
+    }
+    // words whose first bit lies in [lo, hi)
+    const uint64_t w0 = (lo + 31) >> 5, w1 = (hi + 31) >> 5;
+    for (uint64_t w = w0 + threadIdx.x; w < w1; w += blockDim.x) {
+        uint64_t pos = w << 5;
+        uint32_t word = 0;
+        int got = 0;
+        int seg = seg0;
+        while (got < 32 && pos < end) {
+            // advance to the segment holding pos
+            for (;;) {
+                uint64_t s1 = seg < 0 ? (uint64_t)prefix_bits : (seg < nblocks ? offs[seg + 1] : end);
+                if (pos < s1) break;
+                seg++;
+            }
+            uint32_t bitsv;
+            const int take = seg_bits(f, seg, pos, 32 - got, &bitsv);
+            if (take == 0) break;
+            word |= bitsv >> got;
+            got += take;
+            pos += take;
+        }
+        out[w] = bswap32(word);
+    }
+}
+
+}  // namespace bz2mi

@@ -1,0 +1,118 @@
+/*
+ * bz2mi -- MI355X-native bzip2 block compression, C ABI.
+ *
+ * This is the drop-in boundary that replaces the reference's OpenCL device
+ * layer (Stan1slav337/Bzip2-OpenCL include/opencl.hpp Device / Memory<T> /
+ * Kernel, include/kernel.hpp, and the device program kernel.cpp:27-3162).
+ * Plain pointers and sizes only; no exceptions cross it.  Every call returns
+ * BZ2MI_OK (0) or a negative status; bz2mi_last_error() describes the last
+ * failure of the calling thread.  A context is thread-compatible, not
+ * thread-safe: one context per OutputStream, as in the reference.
+ *
+ * Output is bit-identical to the reference's CPU-serial semantics (O_ref,
+ * SURVEY.md section 8c), including the per-slot Huffman seed carry-over that
+ * makes the stream depend on the parallel block count `p`.
+ */
+#ifndef BZ2MI_H
+#define BZ2MI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BZ2MI_OK 0
+#define BZ2MI_EINVAL -1    /* bad argument (reference: std::invalid_argument) */
+#define BZ2MI_EDEVICE -2   /* HIP runtime failure (reference: print_error + exit(1)) */
+#define BZ2MI_ESPACE -3    /* output buffer too small */
+#define BZ2MI_ESTATE -4    /* call out of order (e.g. write after finish) */
+
+typedef struct bz2mi_ctx bz2mi_ctx;
+
+/* Last error message of the calling thread ("" if none). */
+const char* bz2mi_last_error(void);
+
+/* Library / device information. */
+int bz2mi_device_count(void);
+const char* bz2mi_version(void);
+
+/*
+ * Create a compression context on HIP device `device`.
+ *   level           1..9; block size S = unit * level        (OutputStream.hpp:65-77,
+ *                   reference unit = BLOCKSIZE_DEFAULT = 10000, Config.hpp:30)
+ *   parallel_blocks the reference's `p` (>= 1): block b uses Huffman seed slot
+ *                   b mod p (OutputStream.hpp:79-81, 93)
+ *   unit            10000 (reference parity) or 100000 (bzip2-standard 900 KB)
+ * Replaces: OutputStream ctor's Device/Memory/Kernel setup (OutputStream.hpp:83-123,
+ *           opencl.hpp:163-215 Device, :217-459 Memory, :461-539 Kernel).
+ * Returns NULL on failure (see bz2mi_last_error).
+ */
+bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device);
+void bz2mi_destroy(bz2mi_ctx* ctx);
+
+/* Upper bound of the compressed size of n input bytes. */
+size_t bz2mi_compress_bound(size_t n, int level, int unit);
+
+/*
+ * Compress one batch of RLE1 blocks and append the resulting stream bits.
+ * This is OutputStream::closeBlocks (OutputStream.hpp:190-240) around
+ * kernel_close (kernel.cpp:3124-3159): block headers (0x314159265359, CRC,
+ * randomised bit), the device compressor (BWT, MTF/RLE2, Huffman, packing),
+ * and the bit-level stitching with the carried leftover bits.
+ *   blocks  host memory; block j at blocks + j*stride, lens[j] bytes (1..S)
+ *   crcs    block CRCs (BlockCompressor::getCRC, CRC32.hpp:70-73)
+ * The first call also emits the stream header 'BZh'+level (OutputStream.hpp:126-128).
+ * Complete bytes go to out (*out_len set); < 8 pending bits stay in ctx.
+ */
+int bz2mi_compress_rle1(bz2mi_ctx* ctx, const uint8_t* blocks, size_t stride, const uint32_t* lens,
+                        const uint32_t* crcs, uint32_t nblocks, uint8_t* out, size_t cap,
+                        size_t* out_len);
+
+/*
+ * Finish the stream: end-of-stream marker, stream CRC, zero padding
+ * (OutputStream::close, OutputStream.hpp:163-176).  Writes the remaining
+ * bytes to out.  Further compress calls return BZ2MI_ESTATE.
+ */
+int bz2mi_finish(bz2mi_ctx* ctx, uint8_t* out, size_t cap, size_t* out_len);
+
+/*
+ * Block-level entry, the direct analogue of one kernel_close launch
+ * (kernel.cpp:3124-3159) over `nblocks` RLE1 blocks whose stream-global
+ * indices are first_block_index .. +nblocks-1: writes each block's payload
+ * (origPtr .. last data bit, kernel.cpp:3116-3121) packed MSB-first to
+ * out + j*out_stride and its bit count to out_bits[j].  Advances the seed
+ * carry-over state like a batch of the stream.
+ */
+int bz2mi_compress_blocks(bz2mi_ctx* ctx, const uint8_t* blocks, size_t stride, const uint32_t* lens,
+                          uint32_t nblocks, uint8_t* out, size_t out_stride, uint64_t* out_bits);
+
+/*
+ * Whole-stream compression of host bytes (RLE1 front end + device path +
+ * framing): the same bytes the reference's app.cpp writes for this input at
+ * this level and p.  out must hold bz2mi_compress_bound() bytes.
+ */
+int bz2mi_compress(bz2mi_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap,
+                   size_t* out_len);
+
+/*
+ * Device-resident whole-stream compression: d_in / d_out are device pointers
+ * (HBM), `hip_stream` a hipStream_t (NULL = the context's stream).  The RLE1
+ * front end, block split and CRCs run on the device too.  *out_len receives
+ * the stream size.  Used by bench.py with inputs resident in HBM.
+ */
+int bz2mi_compress_device(bz2mi_ctx* ctx, const void* d_in, size_t n, void* d_out, size_t cap,
+                          size_t* out_len, void* hip_stream);
+
+/* Timing of the last device batch, per stage, in milliseconds (HIP events
+ * on the context stream): front, bwt, mtf, seed, huffman, assemble. */
+int bz2mi_last_timings(bz2mi_ctx* ctx, float* ms6);
+
+/* Number of blocks compressed so far in this stream. */
+uint64_t bz2mi_blocks_done(const bz2mi_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
