@@ -57,6 +57,7 @@ struct bz2mi_ctx {
     bool own_stream = false;
     int cap = 0;                 // blocks the batch buffers hold
     int bwt_slots = 0;
+    int batch_blocks = 16384;  // blocks per back-end batch
 
     uint8_t* d_blocks = nullptr;
     uint32_t* d_lens = nullptr;
@@ -79,6 +80,21 @@ struct bz2mi_ctx {
     size_t out_words = 0;
     uint8_t* d_scratch = nullptr;
     uint32_t* d_counter = nullptr;
+    uint32_t* d_crctab = nullptr;
+    // front-end buffers (device RLE1 path)
+    size_t fe_n = 0;
+    uint8_t* d_in = nullptr;        // staging for host input
+    size_t in_cap = 0;
+    uint8_t* d_cost = nullptr;
+    uint8_t* d_dmap = nullptr;
+    uint4* d_summ = nullptr;
+    uint64_t* d_rsb = nullptr;
+    uint32_t* d_ccost = nullptr;
+    uint64_t* d_fc = nullptr;
+    uint64_t* d_bnd = nullptr;
+    uint64_t* d_starts = nullptr;
+    uint64_t* d_nb = nullptr;
+    size_t fe_maxb = 0;
     hipEvent_t ev[8] = {};
     float last_ms[6] = {0, 0, 0, 0, 0, 0};
 
@@ -173,7 +189,11 @@ int run_blocks(bz2mi_ctx* c, int nb) {
     return BZ2MI_OK;
 }
 
-int assemble(bz2mi_ctx* c, int nb, bool final_, uint8_t* out, size_t cap, size_t* out_len) {
+// Lay the stream bits of `nb` compressed blocks (plus prefix: the stream
+// header on the first call, else the carried bits; plus the trailer when
+// final_) into dst as a byte stream.  Returns the total bit count; the last
+// partial byte stays in dst.
+int assemble_to(bz2mi_ctx* c, int nb, bool final_, uint32_t* dst, size_t dst_bytes, uint64_t* total_bits_out) {
     using namespace bz2mi;
     hipStream_t s = c->stream;
     uint64_t prefix = c->carry;
@@ -191,31 +211,160 @@ int assemble(bz2mi_ctx* c, int nb, bool final_, uint8_t* out, size_t cap, size_t
     HIPCHECK(hipStreamSynchronize(s));
     if (final_) end_bits += 80;
     const uint64_t words = (end_bits + 31) / 32;
-    if (words > c->out_words) return fail(BZ2MI_ESPACE, "device output buffer too small");
+    if (words * 4 > dst_bytes) return fail(BZ2MI_ESPACE, "output buffer too small");
     hipLaunchKernelGGL(assemble_kernel, dim3(nb + 2), dim3(256), 0, s, c->d_payload, c->payload_words, c->d_offs,
-                       c->d_crc, nb, prefix, prefix_bits, final_ ? 1 : 0, c->stream_crc, c->d_out);
+                       c->d_crc, nb, prefix, prefix_bits, final_ ? 1 : 0, c->stream_crc, dst);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("assemble");
     HIPCHECK(hipEventRecord(c->ev[5], s));
-    uint64_t total_bits = end_bits;
-    if (final_) total_bits = (total_bits + 7) & ~7ull;  // zero padding
-    const size_t nbytes = (size_t)(total_bits >> 3);
-    const int rem = (int)(total_bits & 7);
-    if (nbytes > cap) return fail(BZ2MI_ESPACE, "output buffer too small");
-    c->h_stage.resize(nbytes + 8);
-    HIPCHECK(hipMemcpyAsync(c->h_stage.data(), c->d_out, nbytes + (rem ? 1 : 0), hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    std::memcpy(out, c->h_stage.data(), nbytes);
-    *out_len = nbytes;
-    c->carry = rem ? ((uint64_t)c->h_stage[nbytes] << 56) & (~0ull << (64 - rem)) : 0;
-    c->carry_bits = rem;
+    *total_bits_out = final_ ? (end_bits + 7) & ~7ull : end_bits;  // final: zero padding
     c->header_done = true;
+    return BZ2MI_OK;
+}
+
+void record_timings(bz2mi_ctx* c, int nb) {
     if (nb > 0) {
         float ms;
         for (int i = 0; i < 5; ++i)
             if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) c->last_ms[i + 1] = ms;
     }
     (void)hipGetLastError();  // timing queries must not leave a sticky error behind
+}
+
+// Assemble into the context's staging buffer and copy complete bytes to host.
+int assemble(bz2mi_ctx* c, int nb, bool final_, uint8_t* out, size_t cap, size_t* out_len) {
+    uint64_t total_bits = 0;
+    int r = assemble_to(c, nb, final_, c->d_out, c->out_words * 4, &total_bits);
+    if (r) return r;
+    const size_t nbytes = (size_t)(total_bits >> 3);
+    const int rem = (int)(total_bits & 7);
+    if (nbytes > cap) return fail(BZ2MI_ESPACE, "output buffer too small");
+    c->h_stage.resize(nbytes + 8);
+    HIPCHECK(hipMemcpyAsync(c->h_stage.data(), c->d_out, nbytes + (rem ? 1 : 0), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    std::memcpy(out, c->h_stage.data(), nbytes);
+    *out_len = nbytes;
+    c->carry = rem ? ((uint64_t)c->h_stage[nbytes] << 56) & (~0ull << (64 - rem)) : 0;
+    c->carry_bits = rem;
+    record_timings(c, nb);
+    return BZ2MI_OK;
+}
+
+int ensure_frontend(bz2mi_ctx* c, size_t n) {
+    if (n <= c->fe_n && c->d_cost) return BZ2MI_OK;
+    const size_t cap = std::max(n, (size_t)1 << 20);
+    const size_t nc = (cap + bz2mi::kFeChunk - 1) / bz2mi::kFeChunk;
+    const size_t maxb = (cap + cap / 4) / (size_t)(c->S - 5) + 8;
+    int r;
+    if ((r = dalloc(&c->d_cost, cap + 64))) return r;
+    if ((r = dalloc(&c->d_dmap, cap + cap / 4 + 4096))) return r;
+    if ((r = dalloc(&c->d_summ, nc + 1))) return r;
+    if ((r = dalloc(&c->d_rsb, nc + 2))) return r;
+    if ((r = dalloc(&c->d_ccost, nc + 1))) return r;
+    if ((r = dalloc(&c->d_fc, nc + 2))) return r;
+    if ((r = dalloc(&c->d_bnd, maxb + 2))) return r;
+    if ((r = dalloc(&c->d_starts, maxb + 3))) return r;
+    if ((r = dalloc(&c->d_nb, 2))) return r;
+    c->fe_n = cap;
+    c->fe_maxb = maxb;
+    return BZ2MI_OK;
+}
+
+void reset_stream(bz2mi_ctx* c) {
+    c->blocks_done = 0;
+    c->stream_crc = 0;
+    c->carry = 0;
+    c->carry_bits = 0;
+    c->header_done = false;
+    c->finished = false;
+    (void)hipMemsetAsync(c->d_state, 0, sizeof(uint32_t) * c->p * bz2mi::kMaxAlpha, c->stream);
+}
+
+// Whole stream from device bytes: front end, back end in block batches,
+// assembly into d_out.  *out_len = stream bytes.
+int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_out, size_t cap, size_t* out_len) {
+    using namespace bz2mi;
+    hipStream_t s = c->stream;
+    int r;
+    reset_stream(c);
+    if ((r = ensure_frontend(c, n))) return r;
+    const uint64_t nc = (n + kFeChunk - 1) / kFeChunk;
+    uint64_t nb = 0;
+    (void)hipGetLastError();
+    HIPCHECK(hipEventRecord(c->ev[6], s));
+    if (n > 0) {
+        const dim3 g4((unsigned)((nc + 3) / 4));
+        hipLaunchKernelGGL(fe_summary_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, c->d_summ);
+        hipLaunchKernelGGL(fe_runscan_kernel, dim3(1), dim3(256), 0, s, c->d_summ, nc, c->d_rsb);
+        hipLaunchKernelGGL(fe_cost_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, c->d_summ, c->d_rsb, c->d_cost,
+                           c->d_ccost);
+        hipLaunchKernelGGL(fe_costscan_kernel, dim3(1), dim3(256), 0, s, c->d_ccost, nc, c->d_fc);
+        hipLaunchKernelGGL(fe_dmap_kernel, g4, dim3(256), 0, s, d_x, c->d_cost, (uint64_t)n, nc, c->d_fc, c->d_dmap);
+        hipLaunchKernelGGL(fe_chain_kernel, dim3(1), dim3(64), 0, s, d_x, c->d_cost, c->d_fc, c->d_summ, c->d_dmap,
+                           (uint64_t)n, nc, c->S, c->d_bnd, (uint64_t)c->fe_maxb, c->d_nb);
+        HIPCHECK(hipGetLastError());
+        STAGE_DONE("front-chain");
+        HIPCHECK(hipMemcpyAsync(&nb, c->d_nb, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        if (nb == 0 || nb > c->fe_maxb) return fail(BZ2MI_EDEVICE, "front end produced an invalid block count");
+        hipLaunchKernelGGL(fe_resolve_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, d_x, c->d_cost, c->d_fc,
+                           c->d_summ, (uint64_t)n, nc, c->d_bnd, c->d_nb, c->d_starts);
+        HIPCHECK(hipGetLastError());
+        STAGE_DONE("front-resolve");
+    }
+    HIPCHECK(hipEventRecord(c->ev[7], s));
+    const uint64_t batch = (uint64_t)c->batch_blocks;
+    size_t o = 0;  // bytes of d_out written
+    std::vector<uint32_t> crcs;
+    for (uint64_t first = 0; first < nb || (nb == 0 && first == 0); first += batch) {
+        const uint64_t cnt = nb ? std::min(batch, nb - first) : 0;
+        const bool last = first + cnt >= nb;
+        if ((r = ensure_capacity(c, (int)std::max<uint64_t>(cnt, 1)))) return r;
+        if (cnt) {
+            hipLaunchKernelGGL(fe_rle1_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts,
+                               first, cnt, c->d_blocks, c->stride, c->d_lens, c->d_crc, c->d_crctab);
+            HIPCHECK(hipGetLastError());
+            STAGE_DONE("front-rle1");
+            if ((r = run_blocks(c, (int)cnt))) return r;
+            crcs.resize(cnt);
+            HIPCHECK(hipMemcpyAsync(crcs.data(), c->d_crc, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            for (uint64_t j = 0; j < cnt; ++j)
+                c->stream_crc = ((c->stream_crc << 1) | (c->stream_crc >> 31)) ^ crcs[j];
+        }
+        // assemble straight into d_out when it is word aligned there, else stage
+        uint64_t bits = 0;
+        const bool direct = o == 0 && c->carry_bits == 0 && ((uintptr_t)d_out & 3) == 0;
+        if (direct) {
+            if ((r = assemble_to(c, (int)cnt, last, (uint32_t*)d_out, cap & ~(size_t)3, &bits))) return r;
+        } else {
+            if ((r = assemble_to(c, (int)cnt, last, c->d_out, c->out_words * 4, &bits))) return r;
+        }
+        const size_t nbytes = (size_t)(bits >> 3);
+        const int rem = (int)(bits & 7);
+        if (o + nbytes + (rem ? 1 : 0) > cap) return fail(BZ2MI_ESPACE, "output buffer too small");
+        if (!direct)
+            HIPCHECK(hipMemcpyAsync(d_out + o, c->d_out, nbytes + (rem ? 1 : 0), hipMemcpyDeviceToDevice, s));
+        if (rem) {
+            uint8_t lastb = 0;
+            HIPCHECK(hipMemcpyAsync(&lastb, d_out + o + nbytes, 1, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            c->carry = ((uint64_t)lastb << 56) & (~0ull << (64 - rem));
+        } else {
+            c->carry = 0;
+        }
+        c->carry_bits = rem;
+        o += nbytes;
+        c->blocks_done += cnt;
+        record_timings(c, (int)cnt);
+        if (nb == 0) break;
+    }
+    HIPCHECK(hipStreamSynchronize(s));
+    float fe_ms = 0;
+    if (hipEventElapsedTime(&fe_ms, c->ev[6], c->ev[7]) == hipSuccess) c->last_ms[0] = fe_ms;
+    (void)hipGetLastError();
+    c->finished = true;
+    *out_len = o;
     return BZ2MI_OK;
 }
 
@@ -287,6 +436,12 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
         return nullptr;
     }
     (void)hipMemset(c->d_state, 0, sizeof(uint32_t) * c->p * bz2mi::kMaxAlpha);
+    if (dalloc(&c->d_crctab, 256) ||
+        hipMemcpy(c->d_crctab, bz2mi::kCrc.t.data(), 256 * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        bz2mi_destroy(c);
+        return nullptr;
+    }
+    if (const char* e = getenv("BZ2MI_BATCH_BLOCKS")) c->batch_blocks = std::max(1, atoi(e));
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     return c;
 }
@@ -297,7 +452,8 @@ void bz2mi_destroy(bz2mi_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_blocks, c->d_lens, c->d_crc, c->d_bwt, c->d_orig, c->d_ranks, c->d_rec, c->d_mtf,
                     c->d_mtflen, c->d_alpha, c->d_hist, c->d_present, c->d_seed, c->d_state, c->d_payload,
-                    c->d_pbits, c->d_offs, c->d_out, c->d_scratch, c->d_counter};
+                    c->d_pbits, c->d_offs, c->d_out, c->d_scratch, c->d_counter, c->d_crctab, c->d_in,
+                    c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd, c->d_starts, c->d_nb};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -380,48 +536,36 @@ int bz2mi_finish(bz2mi_ctx* c, uint8_t* out, size_t cap, size_t* out_len) {
 
 int bz2mi_compress(bz2mi_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
     if (!c || !out_len || (n && !in)) return fail(BZ2MI_EINVAL, "null argument");
-    if (c->finished || c->blocks_done || c->header_done) return fail(BZ2MI_ESTATE, "context already used");
-    // host RLE1 split into batches, device compression per batch
-    const int S = c->S;
-    const size_t hstride = c->stride;
-    const int batch = 4096;
-    std::vector<uint8_t> blocks((size_t)batch * hstride);
-    std::vector<uint32_t> lens(batch), crcs(batch);
-    size_t pos = 0, o = 0;
-    while (pos < n) {
-        int nb = 0;
-        while (nb < batch && pos < n) {
-            bz2mi::Rle1Block blk;
-            blk.begin(blocks.data() + (size_t)nb * hstride, S);
-            pos += blk.put_many(in + pos, n - pos);
-            blk.finish();
-            lens[nb] = (uint32_t)blk.len;
-            crcs[nb] = blk.block_crc();
-            nb++;
-        }
-        size_t got = 0;
-        int r = bz2mi_compress_rle1(c, blocks.data(), hstride, lens.data(), crcs.data(), (uint32_t)nb, out + o,
-                                    cap - o, &got);
+    HIPCHECK(hipSetDevice(c->device));
+    if (n + 64 > c->in_cap) {
+        int r = dalloc(&c->d_in, n + 64);
         if (r) return r;
-        o += got;
+        c->in_cap = n + 64;
     }
+    const size_t dcap = bz2mi_compress_bound(n, c->level, c->unit);
+    uint8_t* d_o = nullptr;
+    HIPCHECK(hipMalloc((void**)&d_o, dcap));
+    int r = BZ2MI_OK;
+    if (n) r = hipMemcpyAsync(c->d_in, in, n, hipMemcpyHostToDevice, c->stream) == hipSuccess
+                   ? BZ2MI_OK : fail(BZ2MI_EDEVICE, "H2D copy failed");
     size_t got = 0;
-    int r = bz2mi_finish(c, out + o, cap - o, &got);
-    if (r) return r;
-    *out_len = o + got;
-    return BZ2MI_OK;
+    if (!r) r = compress_device_impl(c, c->d_in, n, d_o, dcap, &got);
+    if (!r && got > cap) r = fail(BZ2MI_ESPACE, "output buffer too small");
+    if (!r && hipMemcpy(out, d_o, got, hipMemcpyDeviceToHost) != hipSuccess) r = fail(BZ2MI_EDEVICE, "D2H copy failed");
+    (void)hipFree(d_o);
+    if (!r) *out_len = got;
+    return r;
 }
 
 int bz2mi_compress_device(bz2mi_ctx* c, const void* d_in, size_t n, void* d_out, size_t cap, size_t* out_len,
                           void* hip_stream) {
-    (void)c;
-    (void)d_in;
-    (void)n;
-    (void)d_out;
-    (void)cap;
-    (void)out_len;
-    (void)hip_stream;
-    return fail(BZ2MI_EINVAL, "bz2mi_compress_device: not built yet");
+    if (!c || !out_len || (n && !d_in) || !d_out) return fail(BZ2MI_EINVAL, "null argument");
+    HIPCHECK(hipSetDevice(c->device));
+    hipStream_t user = (hipStream_t)hip_stream;
+    if (user) HIPCHECK(hipStreamSynchronize(user));  // inputs written on the caller's stream are complete
+    int r = compress_device_impl(c, (const uint8_t*)d_in, n, (uint8_t*)d_out, cap, out_len);
+    if (r) return r;
+    return BZ2MI_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,615 @@
+// Device RLE1 front end: run-length pre-pass, block split and block CRCs of a
+// raw byte stream resident in HBM.
+//
+// Semantics: BlockCompressor::write / writeRun / finishRLE
+// (reference include/BlockCompressor.hpp:69-154) as driven by
+// OutputStream::write / getNextCompressor (OutputStream.hpp:131-142,
+// 179-188).  A byte is refused by a block once more than S-6 RLE1 bytes have
+// been flushed into it; a flush happens when a run changes value (flushing
+// the previous run's last piece) or when a run piece reaches 255 bytes.
+//
+// Parallel formulation (all per-byte work is data parallel; only the block
+// chain is sequential and it touches one byte per block):
+//   cost(i)  output bytes flushed by the write of byte i in an unsplit stream
+//            (0, or the size 1/2/3/5 of the piece it completes)
+//   Fg(i)    sum of cost(j), j < i      (chunk-level prefix Fc + in-chunk scan)
+//   Ginv(y)  min { i : Fg(i) > y }
+// A block that starts at a run start p ends at E(p) = Ginv(Fg(p+1) + S - 6).
+// D[y] (one byte per output position y) holds Fg(Ginv(y)+1) - y and whether
+// Ginv(y) starts a run, so the chain advances a block per D lookup:
+// y_{k+1} = y_k + D[y_k] + S - 6.  Blocks that start inside a run (rare:
+// the byte after the crossing flush repeats its predecessor) take a slow path
+// that re-phases the run's 255-byte pieces from the block start.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace bz2mi {
+
+namespace {
+
+constexpr int CH = 4096;  // chunk bytes (one wave: 64 lanes x 64 bytes)
+
+__device__ __forceinline__ uint32_t piece_cost(uint32_t len) {  // output bytes of a piece
+    return len >= 4 ? 5u : len;
+}
+
+// 64 bytes of lane `l` of the chunk at c0 (zero beyond n)
+__device__ __forceinline__ void load64(const uint8_t* x, uint64_t n, uint64_t at, uint8_t* v) {
+    if (at + 64 <= n) {
+        const uint4* p = (const uint4*)(x + at);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint4 w = p[q];
+            uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) v[q * 16 + r * 4 + s] = (uint8_t)(ww[r] >> (8 * s));
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 64; ++q) v[q] = (at + q < n) ? x[at + q] : 0;
+    }
+}
+
+}  // namespace
+
+// ---- K1: per-chunk run summary
+__global__ __launch_bounds__(256) void fe_summary_kernel(const uint8_t* __restrict__ x, uint64_t n, uint64_t nc,
+                                                         uint4* __restrict__ summ) {
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
+    if (c >= nc) return;
+    const int lane = lane_id();
+    const uint64_t c0 = c * CH;
+    const uint32_t len = (uint32_t)min((uint64_t)CH, n - c0);
+    const uint64_t at = c0 + (uint64_t)lane * 64;
+    uint8_t v[64];
+    load64(x, n, at, v);
+    const uint32_t prev_last = __shfl_up((uint32_t)v[63], 1);
+    uint32_t first_rs = 0xffffffffu, last_rs = 0;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        const uint32_t pos = (uint32_t)lane * 64 + q;
+        const uint32_t prev = q ? v[q - 1] : prev_last;
+        const bool rs = pos > 0 && pos < len && v[q] != prev;
+        if (rs) {
+            first_rs = min(first_rs, pos);
+            last_rs = pos;
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        first_rs = min(first_rs, (uint32_t)__shfl_xor(first_rs, d));
+        last_rs = max(last_rs, (uint32_t)__shfl_xor(last_rs, d));
+    }
+    if (lane == 0) {
+        const uint32_t lead = first_rs == 0xffffffffu ? len : first_rs;
+        const uint32_t trail = len - last_rs;
+        const uint32_t fb = x[c0], lb = x[c0 + len - 1];
+        summ[c] = make_uint4(fb | (lb << 8), lead, trail, len);
+    }
+}
+
+// ---- K2/K4: single-workgroup scans over chunks
+// rsb[c] = start of the run that holds byte c*CH-1 (c >= 1): an inclusive
+// max-scan of the trailing-run start of every chunk that starts a new run.
+__global__ __launch_bounds__(256) void fe_runscan_kernel(const uint4* __restrict__ summ, uint64_t nc,
+                                                         uint64_t* __restrict__ rsb) {
+    __shared__ uint64_t wtot[4];
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nc; base += 256) {
+        const uint64_t c = base + threadIdx.x;
+        uint64_t own = 0;
+        if (c < nc) {
+            const uint4 sm = summ[c];
+            const uint64_t c0 = c * CH;
+            if (sm.z != sm.w) {
+                own = c0 + sm.w - sm.z;  // trailing run starts inside the chunk
+            } else if (c == 0 || (sm.x & 0xff) != ((summ[c - 1].x >> 8) & 0xff)) {
+                own = c0;                // a one-run chunk that starts a new run
+            }                            // else: the run continues (own = 0)
+        }
+        uint64_t xs = own;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(xs, d);
+            if (lane_id() >= d) xs = xs > y ? xs : y;
+        }
+        if (lane_id() == 63) wtot[wave_id()] = xs;
+        __syncthreads();
+        uint64_t pre = carry;
+        uint64_t all = carry;
+        for (int w = 0; w < 4; ++w) {
+            const uint64_t tw = wtot[w];
+            if (w < wave_id()) pre = pre > tw ? pre : tw;
+            all = all > tw ? all : tw;
+        }
+        const uint64_t incl = xs > pre ? xs : pre;
+        if (c < nc) rsb[c + 1] = incl;
+        carry = uniform64(all);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rsb[0] = 0;
+}
+
+__global__ __launch_bounds__(256) void fe_costscan_kernel(const uint32_t* __restrict__ ccost, uint64_t nc,
+                                                          uint64_t* __restrict__ fc) {
+    __shared__ uint64_t tmp[4];
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nc; base += 256) {
+        const uint64_t c = base + threadIdx.x;
+        const uint64_t v = c < nc ? ccost[c] : 0;
+        uint64_t tot;
+        const uint64_t ex = wg_excl_sum64<256>(v, tmp, &tot);
+        if (c < nc) fc[c] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) fc[nc] = carry;
+}
+
+// ---- K3: per-byte trigger cost
+__global__ __launch_bounds__(256) void fe_cost_kernel(const uint8_t* __restrict__ x, uint64_t n, uint64_t nc,
+                                                      const uint4* __restrict__ summ, const uint64_t* __restrict__ rsb,
+                                                      uint8_t* __restrict__ cost, uint32_t* __restrict__ ccost) {
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
+    if (c >= nc) return;
+    const int lane = lane_id();
+    const uint64_t c0 = c * CH;
+    const uint32_t len = (uint32_t)min((uint64_t)CH, n - c0);
+    const uint64_t at = c0 + (uint64_t)lane * 64;
+    uint8_t v[64];
+    load64(x, n, at, v);
+    const uint32_t prev_last = __shfl_up((uint32_t)v[63], 1);
+    // byte before the chunk
+    const bool chunk_rs = (c == 0) || ((summ[c].x & 0xff) != ((summ[c - 1].x >> 8) & 0xff));
+    // last run start inside this lane (+1; 0 = none), for the carry scan
+    uint64_t lrs = 0;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        const uint32_t pos = (uint32_t)lane * 64 + q;
+        const uint32_t prev = q ? v[q - 1] : prev_last;
+        const bool rs = (pos == 0) ? chunk_rs : (pos < len && v[q] != prev);
+        if (rs && pos < len) lrs = c0 + pos + 1;
+    }
+    uint64_t xs = lrs;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(xs, d);
+        if (lane >= d) xs = xs > y ? xs : y;
+    }
+    uint64_t before = __shfl_up(xs, 1);
+    if (lane == 0) before = 0;
+    // run start in effect before this lane's first byte
+    uint64_t cur = before ? before - 1 : (c == 0 ? 0 : rsb[c]);
+    uint32_t sum = 0;
+    uint32_t packed[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) packed[q] = 0;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        const uint32_t pos = (uint32_t)lane * 64 + q;
+        const uint64_t i = c0 + pos;
+        uint32_t cst = 0;
+        if (pos < len) {
+            const uint32_t prev = q ? v[q - 1] : prev_last;
+            const bool rs = (pos == 0) ? chunk_rs : (v[q] != prev);
+            if (rs) {
+                if (i > 0) {
+                    const uint32_t part = (uint32_t)((i - cur) % 255u);
+                    cst = piece_cost(part);
+                }
+                cur = i;
+            } else if ((i - cur) % 255u == 254u) {
+                cst = 5;
+            }
+        }
+        sum += cst;
+        packed[q >> 2] |= cst << ((q & 3) * 8);
+    }
+    uint4* dst = (uint4*)(cost + at);
+    if (at + 64 <= n) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = make_uint4(packed[4 * q], packed[4 * q + 1], packed[4 * q + 2], packed[4 * q + 3]);
+    } else {
+        for (int q = 0; q < 64; ++q)
+            if (at + q < n) cost[at + q] = (uint8_t)(packed[q >> 2] >> ((q & 3) * 8));
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) ccost[c] = sum;
+}
+
+// ---- K5: D map over output positions
+__global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
+                                                      uint64_t n, uint64_t nc, const uint64_t* __restrict__ fc,
+                                                      uint8_t* __restrict__ dmap) {
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
+    if (c >= nc) return;
+    const int lane = lane_id();
+    const uint64_t c0 = c * CH;
+    const uint64_t at = c0 + (uint64_t)lane * 64;
+    uint8_t v[64], k[64];
+    load64(x, n, at, v);
+    load64(cost, n, at, k);
+    uint32_t lsum = 0;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) lsum += k[q];
+    const uint32_t incl = wave_incl_sum(lsum);
+    uint64_t fg = fc[c] + (incl - lsum);
+    const uint32_t next_v = (at + 64 < n) ? x[at + 64] : 0;
+    const uint32_t next_k = (at + 64 < n) ? cost[at + 64] : 0;
+    for (int q = 0; q < 64; ++q) {
+        const uint64_t i = at + q;
+        const uint32_t ci = k[q];
+        if (ci && i + 2 <= n) {
+            const uint32_t vn = q < 63 ? v[q + 1] : next_v;
+            const uint32_t kn = q < 63 ? k[q + 1] : next_k;
+            const uint32_t rsn = vn != v[q];
+            for (uint32_t r = 0; r < ci; ++r) {
+                const uint32_t d = ci + kn - r;  // Fg(i+2) - y for y = fg + r
+                dmap[fg + r] = (uint8_t)(d | (rsn << 4));
+            }
+        }
+        fg += ci;
+    }
+}
+
+namespace {
+
+struct FeView {
+    const uint8_t* x;
+    const uint8_t* cost;
+    const uint64_t* fc;
+    const uint4* summ;
+    uint64_t n, nc;
+};
+
+// Fg(i) by one wave: chunk prefix + in-chunk sum (all lanes return it)
+__device__ uint64_t fg_at(const FeView& f, uint64_t i) {
+    if (i >= f.n) return f.fc[f.nc];
+    const uint64_t c = i / CH, c0 = c * CH;
+    const int lane = lane_id();
+    uint32_t s = 0;
+    for (uint64_t j = c0 + lane; j < i; j += 64) s += f.cost[j];
+    s = wave_sum(s);
+    return f.fc[c] + s;
+}
+
+// Ginv(y) = min { i : Fg(i) > y } by one wave (binary search over chunks,
+// then an in-chunk scan); returns n if none.
+__device__ uint64_t ginv(const FeView& f, uint64_t y) {
+    if (f.fc[f.nc] <= y) return f.n;
+    // largest c with fc[c] <= y
+    uint64_t lo = 0, hi = f.nc;  // fc[lo] <= y < fc[hi]
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (f.fc[mid] <= y) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t c0 = lo * CH;
+    const int lane = lane_id();
+    const uint64_t at = c0 + (uint64_t)lane * 64;
+    uint32_t ls = 0;
+    for (int q = 0; q < 64; ++q)
+        if (at + q < f.n) ls += f.cost[at + q];
+    const uint32_t incl = wave_incl_sum(ls);
+    const uint64_t base = f.fc[lo] + (incl - ls);
+    // lane whose range holds the first i with Fg(i) > y: Fg(i) = base + prefix up to i
+    // i in (at, at+64]: Fg(at+q+1) = base + sum_{<=q}
+    const uint64_t target = y;
+    uint64_t found = ~0ull;
+    uint64_t run = base;
+    for (int q = 0; q < 64; ++q) {
+        if (at + q >= f.n) break;
+        run += f.cost[at + q];
+        if (run > target) {
+            found = at + q + 1;
+            break;
+        }
+    }
+    // smallest found across lanes
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o = __shfl_xor(found, d);
+        found = o < found ? o : found;
+    }
+    return found == ~0ull ? f.n : found;
+}
+
+// first index > p whose byte differs from x[p] (or n)
+__device__ uint64_t run_end(const FeView& f, uint64_t p) {
+    const uint32_t v = f.x[p];
+    uint64_t at = p + 1;
+    const int lane = lane_id();
+    for (;;) {
+        if (at >= f.n) return f.n;
+        // skip whole chunks that are one run of v
+        const uint64_t c = at / CH;
+        if (at == c * CH && c < f.nc) {
+            const uint4 s = f.summ[c];
+            if (s.z == s.w && (s.x & 0xff) == v) {
+                at += s.w;
+                continue;
+            }
+        }
+        const uint64_t i = at + lane;
+        const bool diff = i >= f.n || f.x[i] != v;
+        const uint64_t m = __ballot(diff);
+        if (m) return at + (uint64_t)(__ffsll((long long)m) - 1);
+        at += 64;
+    }
+}
+
+}  // namespace
+
+// ---- K6: the block chain (one wave).  bnd[k] is the start of block k+1,
+// either as a target y (bit 63 clear: start = Ginv(y)) or as an explicit
+// position (bit 63 set).  *nb_out = number of blocks.
+__global__ __launch_bounds__(64) void fe_chain_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
+                                                      const uint64_t* __restrict__ fc, const uint4* __restrict__ summ,
+                                                      const uint8_t* __restrict__ dmap, uint64_t n, uint64_t nc, int S,
+                                                      uint64_t* __restrict__ bnd, uint64_t max_bnd,
+                                                      uint64_t* __restrict__ nb_out) {
+    FeView f{x, cost, fc, summ, n, nc};
+    const int lane = lane_id();
+    if (n == 0) {
+        if (lane == 0) *nb_out = 0;
+        return;
+    }
+    // Ytot: targets y >= Fg(n-1) have no boundary inside the input
+    const uint64_t ytot = fc[nc] - cost[n - 1];
+    const uint64_t lim = (uint64_t)(S - 6);
+    const uint32_t jstar = (uint32_t)((S - 6) / 5 + 1);
+    uint64_t k = 0;
+    // state: either a target y (case A block) or an explicit mid-run start p
+    bool have_y = true;
+    uint64_t y = lim;   // block 0 starts at 0 (a run start), Fg(1) = 0
+    uint64_t p = 0;
+    for (;;) {
+        if (k + 1 >= max_bnd) break;
+        if (have_y) {
+            if (y >= ytot) break;  // last block
+            const uint32_t d = dmap[y];
+            if (lane == 0) bnd[k] = y;
+            k++;
+            if (d & 16u) {  // next block starts at a run start
+                y = y + (d & 15u) + lim;
+                continue;
+            }
+            p = ginv(f, y);  // next block starts inside a run
+            have_y = false;
+            continue;
+        }
+        // block starting at p, mid-run: its first run is [p, e)
+        const uint64_t e = run_end(f, p);
+        const uint64_t Lr = e - p;
+        if ((uint64_t)jstar * 255u <= Lr) {
+            const uint64_t E = p + (uint64_t)jstar * 255u;
+            if (E >= n) break;
+            if (lane == 0) bnd[k] = E | (1ull << 63);
+            k++;
+            if (E < e) {
+                p = E;  // still inside the run
+                continue;
+            }
+            // E == e: a run start
+            y = fg_at(f, E + 1) + lim;
+            have_y = true;
+            continue;
+        }
+        if (e >= n) break;  // the run reaches the end: last block
+        const uint64_t tot = 5ull * (Lr / 255) + piece_cost((uint32_t)(Lr % 255));
+        if (tot > lim) {
+            const uint64_t E = e + 1;
+            if (E >= n) break;
+            if (lane == 0) bnd[k] = E | (1ull << 63);
+            k++;
+            if (f.x[E] != f.x[E - 1]) {
+                y = fg_at(f, E + 1) + lim;
+                have_y = true;
+            } else {
+                p = E;
+            }
+            continue;
+        }
+        // continue in unsplit coordinates after the run
+        y = fg_at(f, e + 1) - tot + lim;
+        have_y = true;
+    }
+    if (lane == 0) *nb_out = k + 1;
+}
+
+// ---- K7: boundary targets -> positions; starts[0] = 0, starts[nb] = n
+__global__ __launch_bounds__(256) void fe_resolve_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
+                                                         const uint64_t* __restrict__ fc, const uint4* __restrict__ summ,
+                                                         uint64_t n, uint64_t nc, const uint64_t* __restrict__ bnd,
+                                                         const uint64_t* __restrict__ nb_in, uint64_t* __restrict__ starts) {
+    FeView f{x, cost, fc, summ, n, nc};
+    const uint64_t nb = *nb_in;
+    const uint64_t k = (uint64_t)blockIdx.x * 4 + wave_id();
+    if (k == 0 && lane_id() == 0) {
+        starts[0] = 0;
+        starts[nb] = n;
+    }
+    if (k + 1 >= nb) return;
+    const uint64_t b = bnd[k];
+    uint64_t pos;
+    if (b >> 63) pos = b & ~(1ull << 63);
+    else pos = ginv(f, b);
+    if (lane_id() == 0) starts[k + 1] = pos;
+}
+
+namespace {
+
+// CRC register map "process L zero bytes" as 32 columns; apply to v.
+__device__ __forceinline__ uint32_t mat_apply(const uint32_t* col, uint32_t v) {
+    uint32_t r = 0;
+#pragma unroll 8
+    for (int b = 0; b < 32; ++b)
+        if (v >> b & 1u) r ^= col[b];
+    return r;
+}
+
+}  // namespace
+
+// ---- K8: RLE1 emission + block CRC, one workgroup per block
+__global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict__ x, uint64_t n,
+                                                      const uint64_t* __restrict__ starts, uint64_t first, uint64_t count,
+                                                      uint8_t* __restrict__ blocks, size_t stride,
+                                                      uint32_t* __restrict__ lens, uint32_t* __restrict__ crcs,
+                                                      const uint32_t* __restrict__ crc_table) {
+    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t tab[256];
+    __shared__ uint32_t colA[8][32];   // A_{L * 2^l}
+    __shared__ uint32_t colT[32];      // A_len
+    __shared__ uint32_t colW[32];
+    __shared__ uint32_t part[256];
+    __shared__ uint32_t lastv[256];
+    const uint64_t lb = blockIdx.x;  // batch-local block
+    if (lb >= count) return;
+    const uint64_t b = first + lb;
+    const int t = threadIdx.x;
+    tab[t] = crc_table[t];
+    const uint64_t p0 = starts[b], p1 = starts[b + 1];
+    const uint64_t len_in = p1 - p0;
+    uint8_t* out = blocks + lb * stride;
+    // ---- RLE1 emission, tiles of 256 x 16 bytes
+    uint32_t o_carry = 0;
+    uint64_t rs_carry = p0;  // run start in effect before the tile
+    for (uint64_t base = p0; base < p1; base += 4096) {
+        const uint64_t a = base + (uint64_t)t * 16;
+        uint8_t v[16];
+        uint32_t prev = (a > 0 && a - 1 < n) ? x[a - 1] : 0;
+        for (int q = 0; q < 16; ++q) v[q] = (a + q < p1) ? x[a + q] : 0;
+        const uint32_t nextb = (a + 16 < p1) ? x[a + 16] : 0;
+        // last run start (local: i == p0 or x[i] != x[i-1]) inside this thread's bytes
+        uint32_t lrs = 0;  // as offset+1 from p0 (0 = none)
+        for (int q = 0; q < 16; ++q) {
+            const uint64_t i = a + q;
+            if (i < p1) {
+                const uint32_t pv = q ? v[q - 1] : prev;
+                if (i == p0 || v[q] != pv) lrs = (uint32_t)(i - p0) + 1;
+            }
+        }
+        uint32_t tot;
+        const uint32_t mx = wg_incl_max<256>(lrs, tmp, &tot);
+        lastv[t] = mx;
+        __syncthreads();
+        const uint32_t ex = t ? lastv[t - 1] : 0u;  // exclusive max over earlier threads
+        __syncthreads();
+        uint64_t cur = ex ? p0 + ex - 1 : rs_carry;
+        // emission counts
+        uint32_t e = 0;
+        for (int q = 0; q < 16; ++q) {
+            const uint64_t i = a + q;
+            if (i < p1) {
+                const uint32_t pv = q ? v[q - 1] : prev;
+                if (i == p0 || v[q] != pv) cur = i;
+                const uint32_t u = (uint32_t)((i - cur) % 255u);
+                e += u < 3 ? 1u : (u == 3 ? 2u : 0u);
+            }
+        }
+        uint32_t etot;
+        const uint32_t eoff = wg_excl_sum<256>(e, tmp, &etot);
+        // write
+        uint32_t o = o_carry + eoff;
+        cur = ex ? p0 + ex - 1 : rs_carry;
+        for (int q = 0; q < 16; ++q) {
+            const uint64_t i = a + q;
+            if (i < p1) {
+                const uint32_t pv = q ? v[q - 1] : prev;
+                if (i == p0 || v[q] != pv) cur = i;
+                const uint32_t u = (uint32_t)((i - cur) % 255u);
+                const uint32_t nx = q < 15 ? v[q + 1] : nextb;
+                const bool last = (i + 1 == p1) || nx != v[q] || u == 254;
+                if (u < 3) {
+                    out[o++] = v[q];
+                } else if (u == 3) {
+                    out[o] = v[q];
+                    if (last) out[o + 1] = 0;
+                    o += 2;
+                } else if (last) {
+                    out[o - 1] = (uint8_t)(u - 3);
+                }
+            }
+        }
+        o_carry += etot;
+        if (tot) rs_carry = p0 + tot - 1;
+        __syncthreads();
+    }
+    if (t == 0) lens[lb] = o_carry;
+    // ---- block CRC over the input bytes [p0, p1): per-thread crc0 of L bytes
+    // with the range padded at the front by virtual zero bytes (crc0 of
+    // leading zeros is 0), then an ordered tree with A_{L*2^l}.
+    const uint64_t L = (len_in + 255) / 256;
+    const uint64_t pad = L * 256 - len_in;
+    uint32_t r = 0;
+    {
+        const int64_t s0 = (int64_t)((uint64_t)t * L) - (int64_t)pad;
+        for (uint64_t q = 0; q < L; ++q) {
+            const int64_t j = s0 + (int64_t)q;
+            if (j >= 0) r = (r << 8) ^ tab[((r >> 24) ^ x[p0 + (uint64_t)j]) & 0xffu];
+        }
+    }
+    part[t] = r;
+    // A_1 columns, then A_L, A_{2L}, ... by squaring/multiplying (thread k owns column k)
+    __syncthreads();
+    if (t < 32) {
+        const uint32_t e1 = 1u << t;
+        colW[t] = (e1 << 8) ^ tab[e1 >> 24];  // A_1
+    }
+    __syncthreads();
+    // A_L via binary powering: acc = I
+    if (t < 32) colA[0][t] = 1u << t;
+    __syncthreads();
+    for (uint64_t e2 = L; e2; e2 >>= 1) {
+        if (e2 & 1) {
+            uint32_t c = 0;
+            if (t < 32) c = mat_apply(colW, colA[0][t]);
+            __syncthreads();
+            if (t < 32) colA[0][t] = c;
+            __syncthreads();
+        }
+        uint32_t c2 = 0;
+        if (t < 32) c2 = mat_apply(colW, colW[t]);
+        __syncthreads();
+        if (t < 32) colW[t] = c2;
+        __syncthreads();
+    }
+    for (int l = 1; l < 8; ++l) {
+        uint32_t c = 0;
+        if (t < 32) c = mat_apply(colA[l - 1], colA[l - 1][t]);
+        __syncthreads();
+        if (t < 32) colA[l][t] = c;
+        __syncthreads();
+    }
+    // ordered tree: level l combines left (2^l*L bytes) and right: left' = A_{2^l L}(left) ^ right
+    for (int l = 0; l < 8; ++l) {
+        const int stride2 = 1 << (l + 1);
+        uint32_t v = 0;
+        const bool act = (t % stride2) == 0;
+        if (act) v = mat_apply(colA[l], part[t]) ^ part[t + (stride2 >> 1)];
+        __syncthreads();
+        if (act) part[t] = v;
+        __syncthreads();
+    }
+    // A_len for the initial register 0xffffffff
+    if (t < 32) {
+        colT[t] = 1u << t;
+        const uint32_t e1 = 1u << t;
+        colW[t] = (e1 << 8) ^ tab[e1 >> 24];
+    }
+    __syncthreads();
+    for (uint64_t e2 = len_in; e2; e2 >>= 1) {
+        if (e2 & 1) {
+            uint32_t c = 0;
+            if (t < 32) c = mat_apply(colW, colT[t]);
+            __syncthreads();
+            if (t < 32) colT[t] = c;
+            __syncthreads();
+        }
+        uint32_t c2 = 0;
+        if (t < 32) c2 = mat_apply(colW, colW[t]);
+        __syncthreads();
+        if (t < 32) colW[t] = c2;
+        __syncthreads();
+    }
+    if (t == 0) crcs[lb] = ~(mat_apply(colT, 0xffffffffu) ^ part[0]);
+}
+
+}  // namespace bz2mi
