@@ -29,6 +29,7 @@ EXPORTS = (
     "bz2mi_last_error", "bz2mi_device_count", "bz2mi_version", "bz2mi_create", "bz2mi_destroy",
     "bz2mi_compress_bound", "bz2mi_compress_rle1", "bz2mi_finish", "bz2mi_compress_blocks",
     "bz2mi_compress", "bz2mi_compress_device", "bz2mi_last_timings", "bz2mi_blocks_done",
+    "bz2mi_last_stats",
 )
 
 _lib = None
@@ -61,6 +62,8 @@ def lib() -> ctypes.CDLL:
     L.bz2mi_compress_device.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
                                         c.POINTER(c.c_size_t), c.c_void_p]
     L.bz2mi_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
+    L.bz2mi_last_stats.restype = c.c_int
+    L.bz2mi_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
     L.bz2mi_blocks_done.restype = c.c_uint64
     L.bz2mi_blocks_done.argtypes = [c.c_void_p]
     for name in ("bz2mi_compress_rle1", "bz2mi_finish", "bz2mi_compress_blocks", "bz2mi_compress",
@@ -164,6 +167,13 @@ class Context:
         _check(lib().bz2mi_compress_device(self._h, d_in_ptr, n, d_out_ptr, cap, ctypes.byref(out_len),
                                            stream or None))
         return out_len.value
+
+    def stats(self):
+        """Volumes of the last compress_device call (enables collection)."""
+        arr = (ctypes.c_uint64 * 8)()
+        _check(lib().bz2mi_last_stats(self._h, arr))
+        keys = ("input_bytes", "blocks", "rle1_bytes", "mtf_symbols", "payload_bits", "output_bytes", "batch_blocks")
+        return dict(zip(keys, [int(v) for v in list(arr)[:7]]))
 
     def timings(self):
         arr = (ctypes.c_float * 6)()

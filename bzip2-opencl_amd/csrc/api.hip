@@ -58,6 +58,7 @@ struct bz2mi_ctx {
     int cap = 0;                 // blocks the batch buffers hold
     int bwt_slots = 0;
     int batch_blocks = 16384;  // blocks per back-end batch
+    bool want_stats = false;
 
     uint8_t* d_blocks = nullptr;
     uint32_t* d_lens = nullptr;
@@ -97,6 +98,7 @@ struct bz2mi_ctx {
     size_t fe_maxb = 0;
     hipEvent_t ev[8] = {};
     float last_ms[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
     // stream state (OutputStream.hpp:39-44)
     uint64_t blocks_done = 0;
@@ -360,6 +362,28 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
         if (nb == 0) break;
     }
     HIPCHECK(hipStreamSynchronize(s));
+    c->stats[0] = n;
+    c->stats[1] = nb;
+    c->stats[5] = o;
+    if (c->want_stats && nb && nb <= (uint64_t)c->cap) {
+        // per-stage volumes of the last batch (single-batch runs: the whole stream)
+        const uint64_t cnt = nb - (nb - 1) / batch * batch;
+        std::vector<uint32_t> a(cnt), m(cnt);
+        std::vector<uint64_t> pb(cnt);
+        HIPCHECK(hipMemcpy(a.data(), c->d_lens, cnt * 4, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(m.data(), c->d_mtflen, cnt * 4, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(pb.data(), c->d_pbits, cnt * 8, hipMemcpyDeviceToHost));
+        uint64_t sa = 0, sm = 0, sp = 0;
+        for (uint64_t j = 0; j < cnt; ++j) {
+            sa += a[j];
+            sm += m[j];
+            sp += pb[j];
+        }
+        c->stats[2] = sa;
+        c->stats[3] = sm;
+        c->stats[4] = sp;
+        c->stats[6] = cnt;
+    }
     float fe_ms = 0;
     if (hipEventElapsedTime(&fe_ms, c->ev[6], c->ev[7]) == hipSuccess) c->last_ms[0] = fe_ms;
     (void)hipGetLastError();
@@ -463,6 +487,13 @@ void bz2mi_destroy(bz2mi_ctx* c) {
 }
 
 uint64_t bz2mi_blocks_done(const bz2mi_ctx* c) { return c ? c->blocks_done : 0; }
+
+int bz2mi_last_stats(bz2mi_ctx* c, uint64_t* out8) {
+    if (!c || !out8) return fail(BZ2MI_EINVAL, "null argument");
+    c->want_stats = true;  // later device calls also collect the per-stage volumes
+    for (int i = 0; i < 8; ++i) out8[i] = c->stats[i];
+    return BZ2MI_OK;
+}
 
 int bz2mi_last_timings(bz2mi_ctx* c, float* ms6) {
     if (!c || !ms6) return fail(BZ2MI_EINVAL, "null argument");

@@ -109,6 +109,11 @@ int bz2mi_compress_device(bz2mi_ctx* ctx, const void* d_in, size_t n, void* d_ou
  * on the context stream): front, bwt, mtf, seed, huffman, assemble. */
 int bz2mi_last_timings(bz2mi_ctx* ctx, float* ms6);
 
+/* Volumes of the last bz2mi_compress_device call (collected once this has
+ * been called): [0] input bytes, [1] blocks, [2] RLE1 bytes, [3] MTF/RLE2
+ * symbols, [4] payload bits, [5] output bytes, [6] blocks in the last batch. */
+int bz2mi_last_stats(bz2mi_ctx* ctx, uint64_t* out8);
+
 /* Number of blocks compressed so far in this stream. */
 uint64_t bz2mi_blocks_done(const bz2mi_ctx* ctx);
 
