@@ -142,7 +142,7 @@ int ensure_capacity(bz2mi_ctx* c, int nblocks) {
     if ((r = dalloc(&c->d_bwt, B * c->stride))) return r;
     if ((r = dalloc(&c->d_orig, B))) return r;
     if ((r = dalloc(&c->d_ranks, B * c->stride))) return r;
-    if ((r = dalloc(&c->d_rec, B * 64 * 256))) return r;
+    if ((r = dalloc(&c->d_rec, B * 64 * 512))) return r;
     if ((r = dalloc(&c->d_mtf, B * c->mtf_stride))) return r;
     if ((r = dalloc(&c->d_mtflen, B))) return r;
     if ((r = dalloc(&c->d_alpha, B))) return r;

@@ -28,7 +28,6 @@ namespace {
 constexpr int NL = 64;
 
 struct MtfShared {
-    uint32_t lists[NL][64];   // per-lane MTF list, 256 bytes as 64 little-endian words
     uint32_t mask[NL][8];     // per-lane byte set
     uint32_t present[8];
     uint32_t hist[kMaxAlpha];
@@ -55,6 +54,84 @@ __device__ __forceinline__ void emit_run(uint32_t r, uint16_t* out, uint32_t& o)
 }
 
 
+// Result of one lane's MTF pass over its chunk (zero-run boundary state).
+struct LaneRun {
+    uint32_t zl, zt, nz, idig, ia, ib;
+    bool seen_nz;
+};
+
+// Lane-serial move-to-front over [c0, c1) with the list held in W registers
+// (W*4 >= alphabet).  One fused pass per symbol: every word before the match
+// is shifted up one byte (v_alignbyte with the previous word), the matching
+// word is merged up to the match, later words are kept.  When a word has no
+// match, mask = all ones and the merge is the full shift, so the found / not
+// found cases need no branch; a wave-uniform early exit every 8 words stops
+// once every lane has found its symbol.
+template <int W>
+__device__ void mtf_pass(const uint32_t* Lw, const uint8_t* __restrict__ X, uint8_t* __restrict__ R, int c0, int c1,
+                         uint32_t* hist, LaneRun& st) {
+    uint32_t L[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) L[j] = Lw[j];
+    uint32_t run = 0;
+    uint32_t pack = 0;
+    uint32_t xw = 0;
+    for (int i = c0; i < c1; ++i) {
+        if ((i & 3) == 0 || i == c0) xw = *(const uint32_t*)(X + (i & ~3));
+        const uint32_t v = (xw >> ((i & 3) * 8)) & 0xffu;
+        const uint32_t vv = v * 0x01010101u;
+        uint32_t prev = v << 24;
+        bool done = false;
+        uint32_t nbefore = 0, zf = 0;
+        bool all_done = false;
+#pragma unroll
+        for (int g = 0; g < W / 8; ++g) {
+            if (!all_done) {  // wave-uniform: skip the rest once every lane has found its symbol
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) {
+                    const int j = g * 8 + jj;
+                    const uint32_t w = L[j];
+                    const uint32_t x = w ^ vv;
+                    const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
+                    const uint32_t sh = __builtin_amdgcn_alignbyte(w, prev, 3);
+                    const uint32_t lowest = z & (0u - z);
+                    const uint32_t mask = (lowest << 1) - 1u;
+                    const uint32_t merged = (sh & mask) | (w & ~mask);
+                    L[j] = done ? w : merged;
+                    zf = done ? zf : z;
+                    nbefore += done ? 0u : 1u;
+                    done = done || (z != 0u);
+                    prev = w;
+                }
+                all_done = __all(done);
+            }
+        }
+        const uint32_t pos = 4u * (nbefore - 1u) + ((uint32_t)__builtin_ctz(zf) >> 3);
+        pack |= pos << ((i & 3) * 8);
+        if ((i & 3) == 3) {
+            *(uint32_t*)(R + (i & ~3)) = pack;
+            pack = 0;
+        }
+        if (pos == 0) {
+            run++;
+        } else {
+            if (run > 0) {
+                if (st.seen_nz) run_digits(run, st.ia, st.ib, st.idig);
+                else st.zl = run;
+                run = 0;
+            }
+            st.seen_nz = true;
+            st.nz++;
+            atomicAdd(&hist[pos + 1], 1u);
+        }
+    }
+    if (c1 > c0 && (c1 & 3)) *(uint32_t*)(R + (c1 & ~3)) = pack;
+    if (run > 0) {
+        st.zt = run;
+        if (!st.seen_nz) st.zl = run;
+    }
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt, size_t stride,
@@ -71,7 +148,8 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     const int n = (int)lens[b];
     const uint8_t* X = bwt + (size_t)b * stride;
     uint8_t* R = ranks + (size_t)b * stride;
-    uint8_t* myrec = rec + ((size_t)b * NL + c) * 256;
+    // per block: 64 recency lists, then 64 initial MTF lists (256 bytes each)
+    uint8_t* myrec = rec + ((size_t)b * NL * 2 + c) * 256;
     uint16_t* out = mtf_out + (size_t)b * mtf_stride;
 
     int L = (n + NL - 1) / NL;
@@ -102,10 +180,11 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     __syncthreads();
     int k = 0;
     for (int q = 0; q < 8; ++q) k += __popc(sh.present[q]);
+    k = (int)uniform((uint32_t)k);
 
     // ---- 2. initial list of chunk c
     uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t* Lw = sh.lists[c];
+    uint32_t* Lw = (uint32_t*)(rec + ((size_t)b * NL * 2 + NL + c) * 256);
     int len = 0;
     uint32_t word = 0;
     auto push = [&](uint32_t v) {
@@ -117,7 +196,7 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
         len++;
     };
     for (int cc = c - 1; cc >= 0 && len < k; --cc) {
-        const uint8_t* r = rec + ((size_t)b * NL + cc) * 256;
+        const uint8_t* r = rec + ((size_t)b * NL * 2 + cc) * 256;
         int cnt = 0;
         for (int q = 0; q < 8; ++q) cnt += __popc(sh.mask[cc][q]);
         for (int j = 0; j < cnt; ++j) {
@@ -143,50 +222,15 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     }
     if (len & 3) Lw[len >> 2] = word;
 
-    // ---- 3. MTF pass
-    uint32_t zl = 0, zt = 0, nz = 0, run = 0, idig = 0, ia = 0, ib = 0;
-    bool seen_nz = false;
-    uint32_t pack = 0;
-    for (int i = c0; i < c1; ++i) {
-        const uint32_t v = X[i];
-        const uint32_t vv = v * 0x01010101u;
-        uint32_t carry = v;
-        int pos = 0;
-        for (int j = 0; j < 64; ++j) {  // bounded: v is always in the list
-            const uint32_t w = Lw[j];
-            const uint32_t x = w ^ vv;
-            const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
-            const uint32_t sh8 = (w << 8) | carry;
-            if (z) {
-                const int byte = __ffs(z) / 8 - 1;  // first matching byte
-                const uint32_t low = byte == 3 ? 0xffffffffu : ((1u << ((byte + 1) * 8)) - 1u);
-                Lw[j] = (w & ~low) | (sh8 & low);
-                pos = j * 4 + byte;
-                break;
-            }
-            Lw[j] = sh8;
-            carry = w >> 24;
-        }
-        pack |= (uint32_t)pos << ((i & 3) * 8);
-        if ((i & 3) == 3) *(uint32_t*)(R + (i & ~3)) = pack, pack = 0;
-        if (pos == 0) {
-            run++;
-        } else {
-            if (run > 0) {
-                if (seen_nz) run_digits(run, ia, ib, idig);
-                else zl = run;
-                run = 0;
-            }
-            seen_nz = true;
-            nz++;
-            atomicAdd(&sh.hist[pos + 1], 1u);
-        }
-    }
-    if (c1 > c0 && (c1 & 3)) *(uint32_t*)(R + (c1 & ~3)) = pack;
-    if (run > 0) {
-        zt = run;
-        if (!seen_nz) zl = run;
-    }
+    // ---- 3. MTF pass (list in registers; W words cover the k symbols in use)
+    LaneRun st{0, 0, 0, 0, 0, 0, false};
+    if (k <= 32) mtf_pass<8>(Lw, X, R, c0, c1, sh.hist, st);
+    else if (k <= 64) mtf_pass<16>(Lw, X, R, c0, c1, sh.hist, st);
+    else if (k <= 128) mtf_pass<32>(Lw, X, R, c0, c1, sh.hist, st);
+    else mtf_pass<64>(Lw, X, R, c0, c1, sh.hist, st);
+    const uint32_t zl = st.zl, zt = st.zt, nz = st.nz, idig = st.idig, ia = st.ia, ib = st.ib;
+    const bool seen_nz = st.seen_nz;
+    uint32_t run;
     // ---- 4. zero-run ownership and offsets
     const int clen = c1 - c0;
     const uint32_t firstnz = seen_nz ? (uint32_t)(c0 + zl) : (uint32_t)n;
