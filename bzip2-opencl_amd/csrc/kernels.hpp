@@ -8,7 +8,7 @@
 namespace bz2mi {
 
 // Scratch bytes one BWT workgroup slot needs for blocks of S bytes.
-inline size_t bwt_slot_bytes(int S) { return (size_t)40 * (size_t)S + 256; }
+inline size_t bwt_slot_bytes(int S) { return (size_t)48 * (size_t)S + 4096; }
 
 __global__ void bwt_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                            uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,

@@ -24,7 +24,12 @@ for name, e in sorted(man["cases"].items()):
 cref = ctypes.CDLL(os.path.join(REPO, "oracle", "_build", "libcpuref.so"))
 cref.cpuref_compress.restype = ctypes.c_longlong
 cref.cpuref_bound.restype = ctypes.c_size_t
-for gen, n in [(synth.text_bytes, 4 << 20), (synth.random_bytes, 4 << 20), (synth.runs_bytes, 4 << 20)]:
+cases = [(synth.text_bytes, 4 << 20), (synth.random_bytes, 4 << 20), (synth.runs_bytes, 4 << 20),
+         (synth.small_alphabet_bytes, 1 << 20),
+         (lambda n: np.frombuffer((b"ab" * n)[:n], dtype=np.uint8), 300000),
+         (lambda n: np.frombuffer((b"abcab" * n)[:n], dtype=np.uint8), 200000),
+         (lambda n: np.frombuffer((b"the quick brown fox " * n)[:n], dtype=np.uint8), 250000)]
+for gen, n in cases:
     d = gen(n).tobytes()
     cap = cref.cpuref_bound(ctypes.c_size_t(len(d)), 9, 10000)
     out = ctypes.create_string_buffer(cap)
@@ -34,6 +39,6 @@ for gen, n in [(synth.text_bytes, 4 << 20), (synth.random_bytes, 4 << 20), (synt
     ctx = bz2mi.Context(9, 10)
     got = ctx.compress(d)
     dt = time.time() - t
-    print(gen.__name__, len(d), len(ref), len(got), "OK" if got == ref else "DIFF", f"{dt:.2f}s", ctx.timings(), flush=True)
+    print(getattr(gen, "__name__", "lambda"), len(d), len(ref), len(got), "OK" if got == ref else "DIFF", f"{dt:.2f}s", ctx.timings(), flush=True)
     bad += got != ref
 print("BAD", bad)
