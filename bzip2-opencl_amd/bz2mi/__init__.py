@@ -42,6 +42,14 @@ def lib() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"libbz2mi.so not built: run `make -C {os.path.dirname(_HERE)}` ({LIB_PATH})")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7.  If
+    # torch is importable it is loaded first, so libbz2mi's libamdhip64.so.7
+    # dependency binds to that same runtime (same SONAME) and device pointers,
+    # streams and devices are shared; otherwise the system ROCm runtime is used.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     c = ctypes
     L.bz2mi_last_error.restype = c.c_char_p
