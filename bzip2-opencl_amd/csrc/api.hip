@@ -599,4 +599,14 @@ int bz2mi_compress_device(bz2mi_ctx* c, const void* d_in, size_t n, void* d_out,
     return BZ2MI_OK;
 }
 
+// phase stamps of the representative workgroup of the last launch (builds
+// with PHASES=1; returns 0 otherwise): kernel 0 = huffman
+int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
+    if (!out16) return BZ2MI_EINVAL;
+    switch (kernel) {
+        case 0: return bz2mi::huffman_phases(out16);
+        default: return BZ2MI_EINVAL;
+    }
+}
+
 }  // extern "C"

@@ -4,6 +4,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Phase stamps for one representative workgroup (make PHASES=1): a kernel
+// declares a table with BZ2MI_PHASE_TABLE(name) and stamps wall_clock64()
+// (100 MHz) at phase boundaries; bz2mi_debug_phases() reads the tables back.
+#ifdef BZ2MI_PHASES
+#define BZ2MI_PHASE_TABLE(tab) __device__ unsigned long long tab[16];
+#define BZ2MI_PHASE(tab, k, cond)                                   \
+    do {                                                            \
+        if ((cond) && threadIdx.x == 0) tab[k] = wall_clock64();    \
+    } while (0)
+#else
+#define BZ2MI_PHASE_TABLE(tab)
+#define BZ2MI_PHASE(tab, k, cond) \
+    do {                          \
+    } while (0)
+#endif
+
 namespace bz2mi {
 
 // Format constants (reference include/Config.hpp:27-47).

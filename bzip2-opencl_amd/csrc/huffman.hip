@@ -9,94 +9,197 @@
 //   codes      assignHuffmanCodeSymbols          kernel.cpp:2953-2989
 //   tables     writeSelectorsAndHuffmanTables    kernel.cpp:2991-3041
 //   data       writeBlockData                    kernel.cpp:3043-3062
-// Group costs use the six 5-bit code lengths packed into 10-bit lanes of one
-// 64-bit word, so a group's six costs are one add per symbol.  The payload is
-// written MSB-first into a zeroed, byte-swapped 32-bit word image: every
-// thread owns a contiguous bit range (plain stores inside, atomicOr on the two
-// shared end words).
+//
+// Work split (256 threads = 4 waves):
+//  * the two inherently serial pieces -- seed boundaries and the allocator --
+//    run with their array spread over one wave's registers (WaveList): every
+//    access is a readlane (or a lane-select write) with a uniform index
+//    instead of a dependent LDS round trip; tables run on different waves;
+//  * a refinement pass reads each group's 50 symbols once (dword loads),
+//    adds the six packed 10-bit costs per symbol, picks the table and counts
+//    the symbols into that table's frequencies;
+//  * canonical codes, selector MTF positions (from per-table last-use scans)
+//    and table deltas are computed in parallel;
+//  * the data is packed in tiles of 2048 symbols: a workgroup scan of the
+//    code lengths places every thread's 8 codes into an LDS window of the
+//    output, which is flushed as whole words (the partial word carried on).
+// The payload is a byte-swapped 32-bit word image of the MSB-first stream.
 #include "common.hpp"
 #include "kernels.hpp"
 
 namespace bz2mi {
 
+BZ2MI_PHASE_TABLE(g_huf_phase)
+
 namespace {
 
 constexpr int NT = 256;
-constexpr int kMaxSel = 18432;  // >= ceil(900001/50): the 900 KB block mode
+constexpr int NW = NT / 64;
+constexpr int kMaxSel = 18432;                       // >= ceil(900001/50): 900 KB block mode
+constexpr int kTileSyms = 8 * NT;                    // symbols per data tile
+constexpr int kWinWords = kTileSyms * kMaxCodeLen / 32 + 2;
 
 struct HufShared {
-    int lens[kMaxTables][kMaxAlpha];
-    int tf[kMaxTables][kMaxAlpha];
-    int work[kMaxTables][kMaxAlpha];
-    short idx[kMaxTables][kMaxAlpha];
-    uint32_t codes[kMaxTables][kMaxAlpha];
+    uint8_t lens[kMaxTables][kMaxAlpha + 2];
     uint64_t pack[kMaxAlpha];
     uint8_t sel[kMaxSel];
+    union {
+        struct {
+            int tf[kMaxTables][kMaxAlpha];
+            int work[kMaxTables][kMaxAlpha];
+        } opt;
+        struct {
+            uint32_t codes[kMaxTables][kMaxAlpha];
+            uint32_t win[2][kWinWords];
+        } out;
+    } u;
+    uint32_t run[kMaxTables][kMaxCodeLen + 2];
     uint32_t tbits[kMaxTables];
-    uint32_t tmp[NT / 64];
-    uint64_t tmp64[NT / 64];
-    uint64_t bc[4];
+    int lo[kMaxTables], hi[kMaxTables];
+    int last[NW][kMaxTables];
+    int mrg[NW][64];
+    uint32_t tmp[NW];
+};
+
+// ---- an int array of up to 320 entries held in one wave's registers: entry
+// i is lane i%64 of register i/64.  Indices must be wave-uniform.
+struct WaveList {
+    int r0, r1, r2, r3, r4;
+
+    __device__ __forceinline__ void load(const int* src, int n) {
+        const int l = lane_id();
+        r0 = l < n ? src[l] : 0;
+        r1 = l + 64 < n ? src[l + 64] : 0;
+        r2 = l + 128 < n ? src[l + 128] : 0;
+        r3 = l + 192 < n ? src[l + 192] : 0;
+        r4 = l + 256 < n ? src[l + 256] : 0;
+    }
+    // branch-free: read the lane of all five registers, pick with scalar selects
+    __device__ __forceinline__ int get(int i) const {
+        const int k = i >> 6, l = i & 63;
+        const int v0 = __builtin_amdgcn_readlane(r0, l), v1 = __builtin_amdgcn_readlane(r1, l);
+        const int v2 = __builtin_amdgcn_readlane(r2, l), v3 = __builtin_amdgcn_readlane(r3, l);
+        const int v4 = __builtin_amdgcn_readlane(r4, l);
+        return k == 0 ? v0 : k == 1 ? v1 : k == 2 ? v2 : k == 3 ? v3 : v4;
+    }
+    __device__ __forceinline__ void set(int i, int v) {
+        const int k = i >> 6;
+        const bool me = lane_id() == (i & 63);
+        r0 = (me && k == 0) ? v : r0;
+        r1 = (me && k == 1) ? v : r1;
+        r2 = (me && k == 2) ? v : r2;
+        r3 = (me && k == 3) ? v : r3;
+        r4 = (me && k == 4) ? v : r4;
+    }
+    // entries (lo, hi] = v
+    __device__ __forceinline__ void fill(int lo, int hi, int v) {
+        const int l = lane_id();
+        r0 = (l > lo && l <= hi) ? v : r0;
+        r1 = (l + 64 > lo && l + 64 <= hi) ? v : r1;
+        r2 = (l + 128 > lo && l + 128 <= hi) ? v : r2;
+        r3 = (l + 192 > lo && l + 192 <= hi) ? v : r3;
+        r4 = (l + 256 > lo && l + 256 <= hi) ? v : r4;
+    }
 };
 
 // ---- length-limited code length allocator (kernel.cpp:2652-2806), restated
-__device__ int sig_bits(int x) {
-    int n = 0;
-    while (x > 0) {
-        x >>= 1;
-        n++;
-    }
-    return n;
+// over a WaveList.  All values are wave-uniform.
+__device__ __forceinline__ int sig_bits(int x) { return x > 0 ? 32 - __clz(x) : 0; }
+
+// x % len for the entries the allocator takes it of: parent pointers (< 2 len)
+// and depths (< 64); anything else takes the general path.
+__device__ __forceinline__ int mod_len(int x, int len) {
+    if ((unsigned)x < 2u * (unsigned)len) return x >= len ? x - len : x;
+    return x % len;
 }
 
-__device__ int ha_first(const int* a, int len, int i, int nodesToMove) {
+__device__ int ha_first(const WaveList& a, int len, int i, int nodesToMove) {
     const int limit = i;
     int k = len - 2;
-    while (i >= nodesToMove && (a[i] % len) > limit) {
+    while (i >= nodesToMove && mod_len(a.get(i), len) > limit) {
         k = i;
         i -= (limit - i + 1);
     }
     if (i < nodesToMove - 1) i = nodesToMove - 1;
     while (k > i + 1) {
         const int t = (i + k) >> 1;
-        if ((a[t] % len) > limit) k = t;
+        if (mod_len(a.get(t), len) > limit) k = t;
         else i = t;
     }
     return k;
 }
 
-__device__ void ha_allocate(int* a, int len) {
-    if (len <= 2) {
-        if (len == 2) a[1] = 1;
-        a[0] = 1;
-        return;
-    }
-    // extended parent pointers
-    a[0] += a[1];
-    for (int head = 0, tail = 1, top = 2; tail < len - 1; tail++) {
-        int t;
-        if (top >= len || a[head] < a[top]) {
-            t = a[head];
-            a[head++] = tail;
-        } else {
-            t = a[top++];
+// Phase 1 of the allocator: the extended parent pointers of the in-place
+// two-queue Huffman construction (kernel.cpp:2686-2712).  The sequential
+// loop picks items (sorted leaves A[top..], internal nodes IW[head..tail))
+// smallest first -- leaf on ties -- and pairs consecutive picks into the next
+// internal node.  Every internal node made from items >= x weighs >= 2x, so
+// all known items <= 2x are picked, in merged order, before any new one: a
+// wave merges up to 64 of them per step (ranks by binary search across
+// lanes) and forms their pairs at once.  The result is the reference's array:
+// A[k] = parent of internal node k (+len when it was the second pick) for
+// k < len-2, A[len-2] = root weight, A[len-1] = largest leaf.
+__device__ void ha_parents(int* A, int* IW, int* M, int len) {
+    const int lane = lane_id();
+    constexpr int INF = 0x7fffffff;
+    if (lane == 0) IW[0] = A[0] + A[1];
+    int top = 2, head = 0, tail = 1;
+    while (tail < len - 1) {
+        const int li = top + lane, ii = head + lane;
+        const int lw = li < len ? A[li] : INF;
+        const int iw = ii < tail ? IW[ii] : INF;
+        const int x = min(__builtin_amdgcn_readlane(lw, 0), __builtin_amdgcn_readlane(iw, 0));
+        const int limit = 2 * x;  // weights sum to <= 900,001
+        uint64_t bL = __ballot(lw <= limit), bI = __ballot(iw <= limit);
+        int E = (__popcll(bL) + __popcll(bI)) & ~1;
+        if (E > 64) E = 64;
+        if (E == 0) {
+            // only x itself is <= 2x: it pairs with the next smallest known item
+            bL = __ballot(lw != INF);
+            bI = __ballot(iw != INF);
+            E = 2;
         }
-        if (top >= len || (head < tail && a[head] < a[top])) {
-            t += a[head];
-            a[head++] = tail + len;
-        } else {
-            t += a[top++];
+        const int cL = __popcll(bL), cI = __popcll(bI);
+        // merged ranks: leaves before internal nodes of equal weight
+        int nI = 0, nL = 0;  // internal nodes < lw, leaves <= iw
+#pragma unroll
+        for (int step = 64; step > 0; step >>= 1) {
+            const int pi = nI + step - 1, pl = nL + step - 1;
+            const int vi = __shfl(iw, pi & 63), vl = __shfl(lw, pl & 63);
+            if (pi < cI && vi < lw) nI += step;
+            if (pl < cL && vl <= iw) nL += step;
         }
-        a[tail] = t;
+        const int rL = lane + nI, rI = lane + nL;
+        const bool takeL = lane < cL && rL < E, takeI = lane < cI && rI < E;
+        if (takeL) M[rL] = lw;
+        if (takeI) {
+            M[rI] = iw;
+            A[ii] = tail + (rI >> 1) + ((rI & 1) ? len : 0);
+        }
+        const int uL = __popcll(__ballot(takeL)), uI = __popcll(__ballot(takeI));
+        if (lane < (E >> 1)) IW[tail + lane] = M[2 * lane] + M[2 * lane + 1];
+        top += uL;
+        head += uI;
+        tail += E >> 1;
     }
-    // nodes to relocate for the maximum length
+    if (lane == 0) A[len - 2] = IW[len - 2];
+}
+
+// Phase 2 (kernel.cpp:2714-2806): depths from the parent pointers, limited to
+// kMaxCodeLen, written from the top of the array.
+__device__ void ha_depths(WaveList& a, int len) {
     int r = len - 2;
     for (int d = 1; d < kMaxCodeLen - 1 && r > 1; d++) r = ha_first(a, len, r - 1, 0);
-    if ((a[0] % len) >= r) {
+    if (mod_len(a.get(0), len) >= r) {
         int firstNode = len - 2, nextNode = len - 1;
         for (int d = 1, avail = 2; avail > 0 && d < 64; d++) {
             const int lastNode = firstNode;
             firstNode = ha_first(a, len, lastNode - 1, 0);
-            for (int i = avail - (lastNode - firstNode); i > 0; i--) a[nextNode--] = d;
+            const int cnt = avail - (lastNode - firstNode);
+            if (cnt > 0) {
+                a.fill(nextNode - cnt, nextNode, d);
+                nextNode -= cnt;
+            }
             avail = (lastNode - firstNode) << 1;
         }
     } else {
@@ -113,9 +216,13 @@ __device__ void ha_allocate(int* a, int len) {
                 off = left < cap ? left : cap;
             } else if (d == insertDepth - 1) {
                 off = 1;
-                if (a[firstNode] == lastNode) firstNode++;
+                if (a.get(firstNode) == lastNode) firstNode++;
             }
-            for (int i = avail - (lastNode - firstNode + off); i > 0; i--) a[nextNode--] = d;
+            const int cnt = avail - (lastNode - firstNode + off);
+            if (cnt > 0) {
+                a.fill(nextNode - cnt, nextNode, d);
+                nextNode -= cnt;
+            }
             left -= off;
             avail = (lastNode - firstNode + off) << 1;
         }
@@ -126,29 +233,157 @@ __device__ __forceinline__ int table_count(int m) {
     return m >= 2400 ? 6 : m >= 1200 ? 5 : m >= 600 ? 4 : m >= 200 ? 3 : 2;
 }
 
-// code lengths of every table from sh.tf (generateHuffmanCodeLengths)
+// table q is handled by wave q % 4
+__device__ __forceinline__ bool my_table(int q) { return (q & (NW - 1)) == wave_id(); }
+
+// ascending register bitonic sort of 64*E keys over one wave, striped
+// (element e of lane l is item e*64 + l)
+template <int E>
+__device__ __forceinline__ void wave_bitonic32(uint32_t (&key)[8]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j >= 1; j >>= 1) {
+            if (j >= 64) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int pe = e ^ (j / 64);
+                    if (pe > e) {
+                        const bool asc = ((e * 64) & k) == 0;
+                        const uint32_t lo = min(key[e], key[pe]), hi = max(key[e], key[pe]);
+                        key[e] = asc ? lo : hi;
+                        key[pe] = asc ? hi : lo;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const uint32_t o = __shfl_xor(key[e], j);
+                    const bool asc = ((e * 64 + lane) & k) == 0;
+                    const bool lower = (lane & j) == 0;
+                    key[e] = (lower == asc) ? min(key[e], o) : max(key[e], o);
+                }
+            }
+        }
+    }
+}
+
+// code lengths of table q from sh.u.opt.tf[q] (generateHuffmanCodeLengths,
+// kernel.cpp:2835-2857) on one wave: sort the unique keys (freq << 9) | symbol,
+// run the allocator on the sorted frequencies, scatter depths to symbols
+__device__ void build_table(HufShared& sh, int q, int alpha) {
+    const int lane = lane_id();
+    int* tf = sh.u.opt.tf[q];
+    int* A = sh.u.opt.work[q];
+    uint32_t key[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int j = e * 64 + lane;
+        key[e] = j < alpha ? ((uint32_t)tf[j] << 9) | (uint32_t)j : 0xffffffffu;
+    }
+    if (alpha <= 64) wave_bitonic32<1>(key);
+    else if (alpha <= 128) wave_bitonic32<2>(key);
+    else if (alpha <= 256) wave_bitonic32<4>(key);
+    else wave_bitonic32<8>(key);
+#pragma unroll
+    for (int e = 0; e < 5; ++e)
+        if (e * 64 + lane < alpha) A[e * 64 + lane] = (int)(key[e] >> 9);
+    WaveList a;
+    if (alpha > 2) {
+        ha_parents(A, tf, sh.mrg[wave_id()], alpha);  // (tf[q] is free: keys are in registers)
+        a.load(A, alpha);
+        ha_depths(a, alpha);
+    } else {
+        a.load(A, alpha);
+        a.fill(-1, alpha - 1, 1);  // (alpha >= 3 in practice: RUNA, RUNB, EOB)
+    }
+    const int v[5] = {a.r0, a.r1, a.r2, a.r3, a.r4};
+#pragma unroll
+    for (int e = 0; e < 5; ++e)
+        if (e * 64 + lane < alpha) sh.lens[q][key[e] & 511u] = (uint8_t)v[e];
+}
+
+// code lengths of every table, table q on wave q%4
 __device__ void build_lengths(HufShared& sh, int T, int alpha) {
-    const int t = threadIdx.x;
-    // rank sort of the unique keys (freq << 9) | symbol, all tables at once
-    for (int e = t; e < T * alpha; e += NT) {
-        const int q = e / alpha, s = e % alpha;
-        const int key = (sh.tf[q][s] << 9) | s;
-        int r = 0;
-        for (int j = 0; j < alpha; ++j) r += ((sh.tf[q][j] << 9) | j) < key;
-        sh.work[q][r] = key >> 9;
-        sh.idx[q][r] = (short)s;
+    for (int q = 0; q < T; ++q)
+        if (my_table(q)) build_table(sh, q, alpha);
+    __syncthreads();
+}
+
+// exclusive max-scan over the workgroup of six per-thread values (-1 = none)
+__device__ __forceinline__ void wg_excl_max6(int (&v)[kMaxTables], HufShared& sh) {
+    const int lane = lane_id(), w = wave_id();
+    int inc[kMaxTables];
+#pragma unroll
+    for (int u = 0; u < kMaxTables; ++u) {
+        int x = v[u];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d);
+            if (lane >= d) x = max(x, y);
+        }
+        inc[u] = x;
+        if (lane == 63) sh.last[w][u] = x;
     }
     __syncthreads();
-    if (t < T) ha_allocate(sh.work[t], alpha);
-    __syncthreads();
-    for (int e = t; e < T * alpha; e += NT) {
-        const int q = e / alpha, r = e % alpha;
-        sh.lens[q][sh.idx[q][r]] = sh.work[q][r];
+#pragma unroll
+    for (int u = 0; u < kMaxTables; ++u) {
+        int base = -1;
+        for (int k = 0; k < w; ++k) base = max(base, sh.last[k][u]);
+        const int prev = __shfl_up(inc[u], 1);
+        v[u] = max(base, lane ? prev : -1);
     }
     __syncthreads();
 }
 
+// MTF position of selector value v given each table's last use (-1: unused)
+// before it: the list holds the used tables most recent first, then the
+// unused ones ascending (valueToFront, kernel.cpp:3009-3013).
+__device__ __forceinline__ int selector_pos(const int (&last)[kMaxTables], int v) {
+    int lv = last[0];
+#pragma unroll
+    for (int u = 1; u < kMaxTables; ++u) lv = (v == u) ? last[u] : lv;
+    int pos = 0;
+    if (lv >= 0) {
+#pragma unroll
+        for (int u = 0; u < kMaxTables; ++u) pos += last[u] > lv;
+    } else {
+#pragma unroll
+        for (int u = 0; u < kMaxTables; ++u) pos += (last[u] >= 0) | (u < v);
+    }
+    return pos;
+}
+
+__device__ __forceinline__ void note_use(int (&last)[kMaxTables], int v, int g) {
+#pragma unroll
+    for (int u = 0; u < kMaxTables; ++u) last[u] = (v == u) ? g : last[u];
+}
+
+// index of the best (cheapest, first on ties) of T packed 10-bit costs
+__device__ __forceinline__ int best_table(uint64_t c, int T) {
+    int best = 0;
+    uint32_t bestCost = (uint32_t)(c & 1023u);
+    for (int q = 1; q < T; ++q) {
+        const uint32_t cq = (uint32_t)((c >> (10 * q)) & 1023u);
+        if (cq < bestCost) {
+            bestCost = cq;
+            best = q;
+        }
+    }
+    return best;
+}
+
 }  // namespace
+
+int huffman_phases(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_huf_phase), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
+    (void)out;
+    return 0;
+#endif
+}
 
 __global__ __launch_bounds__(256) void huffman_kernel(
     const uint16_t* __restrict__ mtf, size_t mtf_stride, const uint32_t* __restrict__ mtf_len,
@@ -158,101 +393,152 @@ __global__ __launch_bounds__(256) void huffman_kernel(
     __shared__ HufShared sh;
     const int b = blockIdx.x;
     if (b >= nblocks) return;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = lane_id();
     const int m = (int)uniform(mtf_len[b]);
     const int alpha = (int)uniform(alpha_in[b]);
     const int T = table_count(m);
     const int nsel = (m + kGroupRun - 1) / kGroupRun;
     const uint16_t* X = mtf + (size_t)b * mtf_stride;
-    const uint32_t* F = seed + (size_t)b * kMaxAlpha;
     uint32_t* out = payload + (size_t)b * payload_words;
+    const bool stamp = b == nblocks / 2;
+    BZ2MI_PHASE(g_huf_phase, 0, stamp);
 
-    for (int e = t; e < kMaxTables * kMaxAlpha; e += NT) (&sh.lens[0][0])[e] = 0;
-    __syncthreads();
-    // ---- seeds (serial; int32 wrap-around like the reference's int array)
-    if (t == 0) {
+    // ---- seeds: symbol ranges of roughly equal frequency per table (wave 0,
+    // frequencies in registers; int32 wrap-around like the reference's int array)
+    if (wave_id() == 0) {
+        WaveList F;
+        F.load(reinterpret_cast<const int*>(seed + (size_t)b * kMaxAlpha), alpha);
         int32_t remaining = m;
         int lowEnd = -1;
         for (int i = 0; i < T; i++) {
             const int32_t target = remaining / (T - i);
             const int lowStart = lowEnd + 1;
             int32_t actual = 0;
-            while (actual < target && lowEnd < alpha - 1) actual = (int32_t)((uint32_t)actual + F[++lowEnd]);
+            while (actual < target && lowEnd < alpha - 1)
+                actual = (int32_t)((uint32_t)actual + (uint32_t)F.get(++lowEnd));
             if (lowEnd > lowStart && i != 0 && i != T - 1 && ((T - i) % 2) == 0)
-                actual = (int32_t)((uint32_t)actual - F[lowEnd--]);
-            for (int j = 0; j < alpha; j++)
-                if (j < lowStart || j > lowEnd) sh.lens[i][j] = kHighCost;
+                actual = (int32_t)((uint32_t)actual - (uint32_t)F.get(lowEnd--));
+            if (lane == 0) {
+                sh.lo[i] = lowStart;
+                sh.hi[i] = lowEnd;
+            }
             remaining = (int32_t)((uint32_t)remaining - (uint32_t)actual);
         }
     }
     __syncthreads();
-    // ---- 4 refinement passes
+    for (int e = t; e < T * alpha; e += NT) {
+        const int q = e / alpha, j = e - q * alpha;
+        sh.lens[q][j] = (j < sh.lo[q] || j > sh.hi[q]) ? kHighCost : 0;
+    }
+    __syncthreads();
+    BZ2MI_PHASE(g_huf_phase, 1, stamp);
+
+    // ---- 4 refinement passes: choose tables, count, rebuild lengths
     for (int it = 3; it >= 0; --it) {
         for (int s = t; s < alpha; s += NT) {
             uint64_t p = 0;
             for (int q = 0; q < T; ++q) p |= (uint64_t)sh.lens[q][s] << (10 * q);
             sh.pack[s] = p;
         }
-        for (int e = t; e < kMaxTables * kMaxAlpha; e += NT) (&sh.tf[0][0])[e] = 0;
+        for (int e = t; e < kMaxTables * kMaxAlpha; e += NT) (&sh.u.opt.tf[0][0])[e] = 0;
         __syncthreads();
         for (int g = t; g < nsel; g += NT) {
-            const int g0 = g * kGroupRun, g1 = min(g0 + kGroupRun, m);
-            uint64_t c = 0;
-            for (int i = g0; i < g1; ++i) c += sh.pack[X[i]];
-            int best = 0;
-            uint32_t bestCost = (uint32_t)(c & 1023u);
-            for (int q = 1; q < T; ++q) {
-                const uint32_t cq = (uint32_t)((c >> (10 * q)) & 1023u);
-                if (cq < bestCost) {
-                    bestCost = cq;
-                    best = q;
+            const int g0 = g * kGroupRun;
+            if (g0 + kGroupRun <= m) {
+                // 50 symbols = 25 dwords (g0 * 2 bytes is a multiple of 4)
+                const uint32_t* W = reinterpret_cast<const uint32_t*>(X + g0);
+                uint32_t w[kGroupRun / 2];
+#pragma unroll
+                for (int k = 0; k < kGroupRun / 2; ++k) w[k] = W[k];
+                uint64_t c = 0;
+#pragma unroll
+                for (int k = 0; k < kGroupRun / 2; ++k) c += sh.pack[w[k] & 0xffffu] + sh.pack[w[k] >> 16];
+                const int best = best_table(c, T);
+                sh.sel[g] = (uint8_t)best;
+                int* tf = sh.u.opt.tf[best];
+#pragma unroll
+                for (int k = 0; k < kGroupRun / 2; ++k) {
+                    atomicAdd(&tf[w[k] & 0xffffu], 1);
+                    atomicAdd(&tf[w[k] >> 16], 1);
                 }
+            } else {
+                uint64_t c = 0;
+                for (int i = g0; i < m; ++i) c += sh.pack[X[i]];
+                const int best = best_table(c, T);
+                sh.sel[g] = (uint8_t)best;
+                for (int i = g0; i < m; ++i) atomicAdd(&sh.u.opt.tf[best][X[i]], 1);
             }
-            sh.sel[g] = (uint8_t)best;
         }
         __syncthreads();
-        for (int i = t; i < m; i += NT) atomicAdd(&sh.tf[sh.sel[i / kGroupRun]][X[i]], 1);
-        __syncthreads();
+        BZ2MI_PHASE(g_huf_phase, 2 + 2 * (3 - it), stamp);
         build_lengths(sh, T, alpha);
+        BZ2MI_PHASE(g_huf_phase, 3 + 2 * (3 - it), stamp);
     }
-    // ---- canonical codes per table (thread q), table bit sizes
-    if (t < T) {
-        const int* Lq = sh.lens[t];
-        int mn = 32, mx = 0;
-        for (int j = 0; j < alpha; ++j) {
-            mn = Lq[j] < mn ? Lq[j] : mn;
-            mx = Lq[j] > mx ? Lq[j] : mx;
+
+    // ---- canonical codes (assignHuffmanCodeSymbols): codes of length L start
+    // at first[L] = (first[L-1] + count[L-1]) << 1 and go up in symbol order.
+    // Table q on wave q%4; table bit size 5 + sum(2|delta| + 1).
+    for (int q = 0; q < T; ++q) {
+        if (!my_table(q)) continue;
+        const uint8_t* Lq = sh.lens[q];
+        uint32_t cnt = 0, dbits = 0;  // lane L: number of codes of length L
+        for (int j0 = 0; j0 < alpha; j0 += 64) {
+            const int j = j0 + lane;
+            const bool valid = j < alpha;
+            const int L = valid ? Lq[j] : 0;
+            const int d = (valid && j) ? L - Lq[j - 1] : 0;
+            dbits += valid ? 2u * (uint32_t)(d < 0 ? -d : d) + 1u : 0u;
+#pragma unroll
+            for (int k = 1; k <= kMaxCodeLen; ++k) {
+                const uint32_t c = (uint32_t)__popcll(__ballot(valid && L == k));
+                if (lane == k) cnt += c;
+            }
         }
-        uint32_t code = 0;
-        for (int Ln = mn; Ln <= mx; Ln++) {
-            for (int j = 0; j < alpha; j++)
-                if ((Lq[j] & 0xff) == Ln) sh.codes[t][j] = ((uint32_t)Ln << 24) | code++;
-            code <<= 1;
+        dbits = wave_sum(dbits);
+        const uint64_t nz = __ballot(cnt != 0);
+        const int mn = nz ? __ffsll((long long)nz) - 1 : kMaxCodeLen + 1;
+        uint32_t code = 0, myfirst = 0;
+        for (int L = 0; L <= kMaxCodeLen; ++L) {
+            if (lane == L) myfirst = code;
+            if (L >= mn) code = (code + (uint32_t)__builtin_amdgcn_readlane((int)cnt, L)) << 1;
         }
-        uint32_t bits = 5;
-        int cur = Lq[0];
-        for (int j = 0; j < alpha; ++j) {
-            const int d = Lq[j] - cur;
-            bits += 2u * (uint32_t)(d < 0 ? -d : d) + 1u;
-            cur = Lq[j];
+        if (lane < kMaxCodeLen + 2) sh.run[q][lane] = myfirst;
+        if (lane == 0) sh.tbits[q] = 5u + dbits;
+        for (int j0 = 0; j0 < alpha; j0 += 64) {
+            const int j = j0 + lane;
+            const bool valid = j < alpha;
+            const int L = valid ? Lq[j] : 0;
+            const uint64_t peers = wave_match8((uint32_t)L, valid);
+            const uint32_t rank = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+            const uint32_t base = valid ? sh.run[q][L] : 0u;
+            if (valid) sh.u.out.codes[q][j] = ((uint32_t)L << 24) | (base + rank);
+            if (valid && (peers >> lane) == 1ull) sh.run[q][L] = base + rank + 1u;  // highest peer
         }
-        sh.tbits[t] = bits;
     }
-    // ---- selector MTF positions (serial), header size
-    if (t == NT - 1) {
-        uint8_t lst[kMaxTables] = {0, 1, 2, 3, 4, 5};
-        uint64_t sb = 0;
-        for (int g = 0; g < nsel; ++g) {
+
+    // ---- selector MTF positions: every thread walks its contiguous range
+    // knowing, per table, the last use before the range (max-scan)
+    const int sper = (nsel + NT - 1) / NT;
+    const int s0 = min(t * sper, nsel), s1 = min(s0 + sper, nsel);
+    int last0[kMaxTables];
+#pragma unroll
+    for (int u = 0; u < kMaxTables; ++u) last0[u] = -1;
+    for (int g = s0; g < s1; ++g) note_use(last0, sh.sel[g], g);
+    wg_excl_max6(last0, sh);  // (its barriers also complete the codes)
+    uint32_t mysel = 0;
+    {
+        int last[kMaxTables];
+#pragma unroll
+        for (int u = 0; u < kMaxTables; ++u) last[u] = last0[u];
+        for (int g = s0; g < s1; ++g) {
             const int v = sh.sel[g];
-            int pos = 0;
-            while (pos < kMaxTables - 1 && lst[pos] != v) pos++;
-            for (int q = pos; q > 0; q--) lst[q] = lst[q - 1];
-            lst[0] = (uint8_t)v;
-            sb += (uint64_t)pos + 1;
+            mysel += (uint32_t)selector_pos(last, v) + 1u;
+            note_use(last, v, g);
         }
-        sh.bc[0] = sb;
     }
-    __syncthreads();
+    BZ2MI_PHASE(g_huf_phase, 10, stamp);
+    uint32_t selbits;
+    const uint32_t seloff = wg_excl_sum<NT>(mysel, sh.tmp, &selbits);
     // symbol map size
     const uint32_t* P = present + (size_t)b * 8;
     uint32_t used16 = 0;
@@ -263,21 +549,15 @@ __global__ __launch_bounds__(256) void huffman_kernel(
     const uint64_t mapbits = 16 + 16 * (uint64_t)__popc(used16);
     uint64_t tabbits = 0;
     for (int q = 0; q < T; ++q) tabbits += sh.tbits[q];
-    const uint64_t selbits = uniform64(sh.bc[0]);
-    const uint64_t data0 = 24 + mapbits + 3 + 15 + selbits + tabbits;
-    // data size: per-thread contiguous symbol ranges
-    const int per = (m + NT - 1) / NT;
-    const int i0 = min(t * per, m), i1 = min(i0 + per, m);
-    uint64_t mybits = 0;
-    for (int i = i0; i < i1; ++i) mybits += sh.codes[sh.sel[i / kGroupRun]][X[i]] >> 24;
-    uint64_t allbits;
-    const uint64_t myoff = data0 + wg_excl_sum64<NT>(mybits, sh.tmp64, &allbits);
-    const uint64_t total = data0 + allbits;
-    // zero the payload image
-    const uint64_t nwords = (total + 31) / 32 + 1;
-    for (uint64_t w = t; w < nwords; w += NT) out[w] = 0;
+    const uint64_t sel0 = 24 + mapbits + 3 + 15;
+    const uint64_t tab0 = sel0 + selbits;
+    const uint64_t data0 = tab0 + tabbits;
+    const uint64_t dword0 = data0 >> 5;
+    // zero the words before the data (written with atomicOr on shared edges)
+    for (uint64_t w = t; w <= dword0; w += NT) out[w] = 0;
     __syncthreads();
-    // ---- header parts (thread 0): origPtr, symbol map, T, nsel, selectors
+
+    // ---- header (thread 0): origPtr, symbol map, T, nsel
     if (t == 0) {
         BitSink s;
         s.init(out, 0);
@@ -290,49 +570,138 @@ __global__ __launch_bounds__(256) void huffman_kernel(
             }
         s.put(3, (uint32_t)T);
         s.put(15, (uint32_t)nsel);
-        uint8_t lst[kMaxTables] = {0, 1, 2, 3, 4, 5};
-        for (int g = 0; g < nsel; ++g) {
-            const int v = sh.sel[g];
-            int pos = 0;
-            while (pos < kMaxTables - 1 && lst[pos] != v) pos++;
-            for (int q = pos; q > 0; q--) lst[q] = lst[q - 1];
-            lst[0] = (uint8_t)v;
-            s.put(pos + 1, ((1u << pos) - 1u) << 1);  // writeUnary: pos ones, then a zero
-        }
         s.finish();
     }
-    // tables: thread 64+q writes table q
-    if (t >= 64 && t < 64 + T) {
-        const int q = t - 64;
-        uint64_t at = 24 + mapbits + 18 + selbits;
-        for (int r = 0; r < q; ++r) at += sh.tbits[r];
-        BitSink s;
-        s.init(out, at);
-        const int* Lq = sh.lens[q];
-        int cur = Lq[0];
-        s.put(5, (uint32_t)cur);
-        for (int j = 0; j < alpha; ++j) {
-            const int L = Lq[j];
-            int d = L - cur;
-            const uint32_t v = d > 0 ? 2u : 3u;  // 10 = +1, 11 = -1
-            if (d < 0) d = -d;
-            while (d-- > 0) s.put(2, v);
-            s.put(1, 0);
-            cur = L;
-        }
-        s.finish();
-    }
-    // data: every thread its range
+    // ---- selectors (writeUnary: pos ones, then a zero), every thread its range
     {
         BitSink s;
-        s.init(out, myoff);
-        for (int i = i0; i < i1; ++i) {
-            const uint32_t cs = sh.codes[sh.sel[i / kGroupRun]][X[i]];
-            s.put((int)(cs >> 24), cs & 0xffffffu);
+        s.init(out, sel0 + seloff);
+        int last[kMaxTables];
+#pragma unroll
+        for (int u = 0; u < kMaxTables; ++u) last[u] = last0[u];
+        for (int g = s0; g < s1; ++g) {
+            const int v = sh.sel[g];
+            const int pos = selector_pos(last, v);
+            s.put(pos + 1, ((1u << pos) - 1u) << 1);
+            note_use(last, v, g);
         }
         s.finish();
     }
-    if (t == 0) payload_bits[b] = total;
+    // ---- tables (delta-coded lengths): table q on wave q%4, one symbol per
+    // lane -- its |delta| pairs (10 = +1, 11 = -1) and the closing 0 -- placed
+    // by a wave scan of the piece lengths
+    for (int q = 0; q < T; ++q) {
+        if (!my_table(q)) continue;
+        uint64_t at = tab0;
+        for (int r = 0; r < q; ++r) at += sh.tbits[r];
+        const uint8_t* Lq = sh.lens[q];
+        if (lane == 0) put_bits_or(out, at, 5, Lq[0]);
+        at += 5;
+        for (int j0 = 0; j0 < alpha; j0 += 64) {
+            const int j = j0 + lane;
+            const bool valid = j < alpha;
+            const int d = (valid && j) ? (int)Lq[j] - (int)Lq[j - 1] : 0;
+            const int ad = d < 0 ? -d : d;
+            const uint32_t nb = valid ? 2u * (uint32_t)ad + 1u : 0u;
+            const uint32_t inc = wave_incl_sum(nb);
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            if (valid) {
+                const uint64_t pat = d > 0 ? 0xaaaaaaaaaaaaaaaaull : ~0ull;
+                const uint64_t v = (pat & ((1ull << (2 * ad)) - 1ull)) << 1;
+                const uint64_t p = at + inc - nb;
+                if (nb > 32) {
+                    put_bits_or(out, p, (int)nb - 32, (uint32_t)(v >> 32));
+                    put_bits_or(out, p + nb - 32, 32, (uint32_t)v);
+                } else {
+                    put_bits_or(out, p, (int)nb, (uint32_t)v);
+                }
+            }
+            at += total;
+        }
+    }
+    BZ2MI_PHASE(g_huf_phase, 11, stamp);
+
+    // ---- data (writeBlockData): tiles of 2048 symbols, 8 per thread, packed
+    // into an LDS window of the stream and flushed as whole words
+    for (int k = t; k < 2 * kWinWords; k += NT) (&sh.u.out.win[0][0])[k] = 0;
+    __syncthreads();
+    uint64_t bit0 = data0;  // stream position of the current tile
+    int cur = 0;
+    for (int base = 0; base < m; base += kTileSyms) {
+        const int i0 = base + 8 * t;
+        uint32_t sym[8];
+        if (i0 + 8 <= m) {
+            const uint4 v = *reinterpret_cast<const uint4*>(X + i0);
+            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                sym[2 * k] = vv[k] & 0xffffu;
+                sym[2 * k + 1] = vv[k] >> 16;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sym[k] = i0 + k < m ? X[i0 + k] : 0u;
+        }
+        uint32_t cs[8];
+        uint32_t mybits = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k;
+            cs[k] = i < m ? sh.u.out.codes[sh.sel[(unsigned)i / kGroupRun]][sym[k]] : 0u;
+            mybits += cs[k] >> 24;
+        }
+        uint32_t tilebits;
+        const uint32_t off = wg_excl_sum<NT>(mybits, sh.tmp, &tilebits);
+        uint32_t* win = sh.u.out.win[cur];
+        const uint64_t w0 = bit0 >> 5;
+        {
+            const uint32_t p = (uint32_t)(bit0 & 31) + off;
+            uint32_t wi = p >> 5;
+            int nacc = (int)(p & 31);
+            uint64_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int L = (int)(cs[k] >> 24);
+                acc |= ((uint64_t)(cs[k] & 0xffffffu) << (63 - L) << 1) >> nacc;
+                nacc += L;
+                if (nacc >= 32) {
+                    atomicOr(&win[wi], (uint32_t)(acc >> 32));
+                    acc <<= 32;
+                    nacc -= 32;
+                    wi++;
+                }
+            }
+            if (nacc > 0) atomicOr(&win[wi], (uint32_t)(acc >> 32));
+        }
+        __syncthreads();
+        const uint64_t bit1 = bit0 + tilebits;
+        const int nfull = (int)((bit1 >> 5) - w0);
+        uint32_t* nxt = sh.u.out.win[cur ^ 1];
+        for (int k = t; k <= nfull; k += NT) {
+            const uint32_t v = win[k];
+            win[k] = 0;
+            if (k == nfull) nxt[0] = v;  // partial word carried into the next tile
+            else if (w0 + k == dword0) atomicOr(&out[w0 + k], bswap32(v));
+            else out[w0 + k] = bswap32(v);
+        }
+        bit0 = bit1;
+        cur ^= 1;
+        // (the next tile's scan barriers order these window writes)
+    }
+    __syncthreads();
+    // last partial word, and a zero word after the stream
+    if (t == 0) {
+        const uint64_t wl = bit0 >> 5;
+        const uint32_t v = sh.u.out.win[cur][0];
+        if (wl == dword0) atomicOr(&out[wl], bswap32(v));
+        else out[wl] = bswap32(v);
+        if (bit0 & 31) out[wl + 1] = 0;
+        payload_bits[b] = bit0;
+    }
+#ifdef BZ2MI_PHASES
+    __syncthreads();
+    BZ2MI_PHASE(g_huf_phase, 12, stamp);
+#endif
 }
 
 }  // namespace bz2mi

@@ -1,0 +1,31 @@
+"""Phase stamps of one representative workgroup per kernel (libbz2mi built
+with `make PHASES=1`): runs one compression of 256 MiB random bytes and prints
+per-phase microseconds."""
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bzip2-opencl_amd"))
+import torch
+import bz2mi
+
+n = int(os.environ.get("MIB", "256")) << 20
+kind = os.environ.get("DATA", "random")
+g = torch.Generator(device="cuda").manual_seed(0x5EED0001)
+if kind == "random":
+    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+else:
+    from bz2mi import synth
+    x = torch.from_numpy(synth.text_bytes(n)).cuda()
+ctx = bz2mi.Context(9, 10)
+out = torch.empty(n + n // 8 + (1 << 20), dtype=torch.uint8, device="cuda")
+for _ in range(2):
+    ctx.compress_device(x.data_ptr(), n, out.data_ptr(), out.numel())
+torch.cuda.synchronize()
+L = bz2mi.lib()
+buf = (ctypes.c_ulonglong * 16)()
+for k, name in [(0, "huffman")]:
+    r = L.bz2mi_debug_phases(k, buf)
+    v = list(buf)
+    print(name, "rc", r, "us:", [round((v[i + 1] - v[i]) / 100.0, 1) if v[i] and v[i + 1] else None for i in range(15) if v[i + 1]],
+          "total", round((max(v) - v[0]) / 100.0, 1))
+print("timings", ctx.timings())
+if len(v) > 14 and v[13] and v[14]:
+    print("last build_lengths: rank sort", round((v[13] - v[8]) / 100.0, 1), "allocator", round((v[14] - v[13]) / 100.0, 1))
