@@ -74,6 +74,11 @@ def lib() -> ctypes.CDLL:
     L.bz2mi_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
     L.bz2mi_blocks_done.restype = c.c_uint64
     L.bz2mi_blocks_done.argtypes = [c.c_void_p]
+    # debugging entry points (not in include/bz2mi.h)
+    L.bz2mi_debug_selftest.restype = c.c_int
+    L.bz2mi_debug_selftest.argtypes = [c.POINTER(c.c_uint32), c.c_int]
+    L.bz2mi_debug_phases.restype = c.c_int
+    L.bz2mi_debug_phases.argtypes = [c.c_int, c.POINTER(c.c_ulonglong)]
     for name in ("bz2mi_compress_rle1", "bz2mi_finish", "bz2mi_compress_blocks", "bz2mi_compress",
                  "bz2mi_compress_device", "bz2mi_last_timings"):
         getattr(L, name).restype = c.c_int

@@ -600,13 +600,24 @@ int bz2mi_compress_device(bz2mi_ctx* c, const void* d_in, size_t n, void* d_out,
 }
 
 // phase stamps of the representative workgroup of the last launch (builds
-// with PHASES=1; returns 0 otherwise): kernel 0 = huffman
+// with PHASES=1; returns 0 otherwise): kernel 0 = huffman, 1 = bwt, 2 = mtf,
+// 3 = front end
 int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
     if (!out16) return BZ2MI_EINVAL;
     switch (kernel) {
         case 0: return bz2mi::huffman_phases(out16);
+        case 1: return bz2mi::bwt_phases(out16);
+        case 2: return bz2mi::mtf_phases(out16);
+        case 3: return bz2mi::fe_phases(out16);
         default: return BZ2MI_EINVAL;
     }
+}
+
+// device self-test of the cross-lane primitives: fills bad[0..9] with
+// mismatch counts (all zero on a healthy build); returns the number of checks
+int bz2mi_debug_selftest(uint32_t* bad, int n) {
+    if (!bad || n < 10) return BZ2MI_EINVAL;
+    return bz2mi::run_selftest(bad, n);
 }
 
 }  // extern "C"

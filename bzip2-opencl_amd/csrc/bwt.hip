@@ -29,6 +29,17 @@
 
 namespace bz2mi {
 
+BZ2MI_PHASE_TABLE(g_bwt_phase)
+
+int bwt_phases(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwt_phase), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
+    (void)out;
+    return 0;
+#endif
+}
+
 namespace {
 
 constexpr int NT = 256;
@@ -426,8 +437,9 @@ __device__ void wg_partition(const uint8_t* __restrict__ T, int n, Scratch& s, S
 }
 
 __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restrict__ out, uint32_t* __restrict__ orig,
-                          Scratch& s, BwtShared& sh) {
+                          Scratch& s, BwtShared& sh, bool stamp) {
     const int t = threadIdx.x;
+    BZ2MI_PHASE(g_bwt_phase, 0, stamp);
     // ---- phase 1a: counting sort by the first byte
     sh.hist[t] = 0;
     if (t < 8) sh.cnt[t] = 0;
@@ -449,6 +461,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
         }
         __syncthreads();
     }
+    BZ2MI_PHASE(g_bwt_phase, 1, stamp);
     // ---- phase 1b: levels of (small sorts, large partitions)
     uint32_t depth = 1;
     Seg* large = s.large;
@@ -466,6 +479,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
             wave_sort_any(T, n, s, s.small[idx], depth, 0, s.grp, &sh.cnt[2]);
         }
         __syncthreads();
+        BZ2MI_PHASE(g_bwt_phase, 2, stamp && depth == 1);
         const uint32_t nlarge = uniform(sh.cnt[1]);
         if (nlarge == 0) break;
         if (t == 0) {
@@ -481,6 +495,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
         large_next = tmpl;
         depth++;
     }
+    BZ2MI_PHASE(g_bwt_phase, 3, stamp);
     // ---- phase 2: prefix doubling on the unresolved groups
     Seg* g = s.grp;
     Seg* g2 = s.grp2;
@@ -528,6 +543,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
         g2 = tg;
         __syncthreads();
     }
+    BZ2MI_PHASE(g_bwt_phase, 4, stamp);
     // ---- BWT bytes and origPtr
     for (int k = t; k < n; k += NT) {
         const uint32_t i = s.sa[k];
@@ -535,6 +551,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
         if (i == 0) *orig = (uint32_t)k;
     }
     __syncthreads();
+    BZ2MI_PHASE(g_bwt_phase, 5, stamp);
 }
 
 }  // namespace
@@ -559,7 +576,7 @@ __global__ __launch_bounds__(256) void bwt_kernel(const uint8_t* __restrict__ bl
         uint8_t* out = bwt_out + (size_t)b * stride;
         const int n = __builtin_amdgcn_readfirstlane((int)lens[b]);
         if (n > 1) {
-            bwt_block(T, n, out, orig_out + b, s, sh);
+            bwt_block(T, n, out, orig_out + b, s, sh, b == nblocks / 2);
         } else if (t == 0) {
             if (n == 1) out[0] = T[0];
             orig_out[b] = 0;

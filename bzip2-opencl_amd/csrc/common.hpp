@@ -47,14 +47,89 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// Inclusive scans over one 64-lane wave.
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
+// ---- cross-lane moves without the LDS crossbar (ds_bpermute): DPP row /
+// quad permutes and the gfx950 permlane swaps, all plain VALU ops.
+namespace dpp {
+constexpr int kQuadXor1 = 0xB1;    // quad_perm [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;    // quad_perm [2,3,0,1]
+constexpr int kQuadXor3 = 0x1B;    // quad_perm [3,2,1,0]
+constexpr int kRowShr1 = 0x111;    // row_shr:n = 0x110 + n
+constexpr int kRowRor8 = 0x128;    // row_ror:8 (= xor 8 inside a row of 16)
+constexpr int kWaveShr1 = 0x138;   // wave_shr:1
+constexpr int kHalfMirror = 0x141; // row_half_mirror (= xor 7 inside 8 lanes)
+constexpr int kBcast15 = 0x142;    // row_bcast:15
+constexpr int kBcast31 = 0x143;    // row_bcast:31
+}  // namespace dpp
+
+template <int Ctrl, int RowMask = 0xf>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v, uint32_t old = 0) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, Ctrl, RowMask, 0xf, false);
+}
+
+// value of lane (lane ^ J), J a power of two < 64
+template <int J>
+__device__ __forceinline__ uint32_t xor_lanes(uint32_t v) {
+    if constexpr (J == 1) {
+        return dpp_mov<dpp::kQuadXor1>(v);
+    } else if constexpr (J == 2) {
+        return dpp_mov<dpp::kQuadXor2>(v);
+    } else if constexpr (J == 4) {
+        return dpp_mov<dpp::kQuadXor3>(dpp_mov<dpp::kHalfMirror>(v));
+    } else if constexpr (J == 8) {
+        return dpp_mov<dpp::kRowRor8>(v);
+    } else if constexpr (J == 16) {
+        // swaps the odd rows of the first operand with the even rows of the second
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (threadIdx.x & 16) ? r[0] : r[1];
+    } else {
+        static_assert(J == 32, "xor_lanes: J in {1,2,4,8,16,32}");
+        // swaps the upper half of the first operand with the lower half of the second
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32) ? r[0] : r[1];
     }
+}
+
+__device__ __forceinline__ uint32_t xor_lanes_rt(uint32_t v, int j) {
+    switch (j) {
+        case 1: return xor_lanes<1>(v);
+        case 2: return xor_lanes<2>(v);
+        case 4: return xor_lanes<4>(v);
+        case 8: return xor_lanes<8>(v);
+        case 16: return xor_lanes<16>(v);
+        default: return xor_lanes<32>(v);
+    }
+}
+
+__device__ __forceinline__ uint64_t xor_lanes_rt64(uint64_t v, int j) {
+    const uint32_t lo = xor_lanes_rt((uint32_t)v, j), hi = xor_lanes_rt((uint32_t)(v >> 32), j);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// value of lane - 1 (lane 0 gets `first`)
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v, uint32_t first = 0) {
+    const uint32_t p = dpp_mov<dpp::kWaveShr1>(v);
+    return lane_id() ? p : first;
+}
+
+// Inclusive scans over one 64-lane wave: row_shr 1,2,4,8 inside rows of 16,
+// then row_bcast15 / row_bcast31 carry across rows.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += dpp_mov<dpp::kRowShr1>(x);
+    x += dpp_mov<dpp::kRowShr1 + 1>(x);
+    x += dpp_mov<dpp::kRowShr1 + 3>(x);
+    x += dpp_mov<dpp::kRowShr1 + 7>(x);
+    x += dpp_mov<dpp::kBcast15, 0xa>(x);
+    x += dpp_mov<dpp::kBcast31, 0xc>(x);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp_mov<dpp::kRowShr1>(x));
+    x = max(x, dpp_mov<dpp::kRowShr1 + 1>(x));
+    x = max(x, dpp_mov<dpp::kRowShr1 + 3>(x));
+    x = max(x, dpp_mov<dpp::kRowShr1 + 7>(x));
+    x = max(x, dpp_mov<dpp::kBcast15, 0xa>(x));
+    x = max(x, dpp_mov<dpp::kBcast31, 0xc>(x));
     return x;
 }
 
@@ -68,20 +143,8 @@ __device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t x) {
     return x;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x = x > y ? x : y;
-    }
-    return x;
-}
-
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-    return x;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(x), 63);
 }
 
 // Exclusive sum over a workgroup of NT threads.  `tmp` needs NT/64 words of

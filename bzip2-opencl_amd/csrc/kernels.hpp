@@ -21,7 +21,11 @@ __global__ void mtf_kernel(const uint8_t* bwt, size_t stride, const uint32_t* le
 __global__ void seed_kernel(const uint32_t* hist, uint32_t* seed, uint32_t* state, int nblocks, int p,
                             uint64_t first_block);
 
-int huffman_phases(unsigned long long* out);  // phase stamps (make PHASES=1)
+int huffman_phases(unsigned long long* out);
+int bwt_phases(unsigned long long* out);
+int mtf_phases(unsigned long long* out);
+int fe_phases(unsigned long long* out);
+int run_selftest(uint32_t* host_bad, int n);  // cross-lane primitive checks  // phase stamps (make PHASES=1)
 __global__ void huffman_kernel(const uint16_t* mtf, size_t mtf_stride, const uint32_t* mtf_len,
                                const uint32_t* alpha_in, const uint32_t* seed, const uint32_t* present,
                                const uint32_t* orig, int nblocks, uint32_t* payload, size_t payload_words,

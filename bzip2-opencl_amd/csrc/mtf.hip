@@ -134,6 +134,17 @@ __device__ void mtf_pass(const uint32_t* Lw, const uint8_t* __restrict__ X, uint
 
 }  // namespace
 
+BZ2MI_PHASE_TABLE(g_mtf_phase)
+
+int mtf_phases(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mtf_phase), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
+    (void)out;
+    return 0;
+#endif
+}
+
 __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt, size_t stride,
                                                  const uint32_t* __restrict__ lens, int nblocks,
                                                  uint8_t* __restrict__ ranks, uint8_t* __restrict__ rec,
@@ -151,6 +162,8 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     // per block: 64 recency lists, then 64 initial MTF lists (256 bytes each)
     uint8_t* myrec = rec + ((size_t)b * NL * 2 + c) * 256;
     uint16_t* out = mtf_out + (size_t)b * mtf_stride;
+    const bool stamp = b == nblocks / 2;
+    BZ2MI_PHASE(g_mtf_phase, 0, stamp);
 
     int L = (n + NL - 1) / NL;
     L = (L + 3) & ~3;
@@ -182,6 +195,7 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     for (int q = 0; q < 8; ++q) k += __popc(sh.present[q]);
     k = (int)uniform((uint32_t)k);
 
+    BZ2MI_PHASE(g_mtf_phase, 1, stamp);
     // ---- 2. initial list of chunk c
     uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t* Lw = (uint32_t*)(rec + ((size_t)b * NL * 2 + NL + c) * 256);
@@ -222,6 +236,8 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     }
     if (len & 3) Lw[len >> 2] = word;
 
+    __syncthreads();
+    BZ2MI_PHASE(g_mtf_phase, 2, stamp);
     // ---- 3. MTF pass (list in registers; W words cover the k symbols in use)
     LaneRun st{0, 0, 0, 0, 0, 0, false};
     if (k <= 32) mtf_pass<8>(Lw, X, R, c0, c1, sh.hist, st);
@@ -231,6 +247,8 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     const uint32_t zl = st.zl, zt = st.zt, nz = st.nz, idig = st.idig, ia = st.ia, ib = st.ib;
     const bool seen_nz = st.seen_nz;
     uint32_t run;
+    __syncthreads();
+    BZ2MI_PHASE(g_mtf_phase, 3, stamp);
     // ---- 4. zero-run ownership and offsets
     const int clen = c1 - c0;
     const uint32_t firstnz = seen_nz ? (uint32_t)(c0 + zl) : (uint32_t)n;
@@ -295,6 +313,7 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
         if (run > 0) emit_run(lead ? lead_len : tail_len, out, o);
     }
     __syncthreads();
+    BZ2MI_PHASE(g_mtf_phase, 4, stamp);
     const uint32_t eob = (uint32_t)k + 1;
     if (c == NL - 1) {
         out[total] = (uint16_t)eob;

@@ -29,6 +29,16 @@ def bz():
     return bz2mi
 
 
+def test_cross_lane_primitives(bz):
+    """DPP / permlane moves and DPP wave scans agree with ds_bpermute shuffles
+    and serial sums (the sorts and scans of every kernel build on them)."""
+    bad = (ctypes.c_uint32 * 16)()
+    L = bz.lib()
+    assert L.bz2mi_debug_selftest(bad, 16) == 10
+    names = ["xor1", "xor2", "xor4", "xor8", "xor16", "xor32", "lane_prev", "incl_sum", "incl_max", "wave_sum"]
+    assert {n: bad[i] for i, n in enumerate(names) if bad[i]} == {}, " ".join(str(x) for x in bad)
+
+
 def test_golden_streams(bz, manifest):
     for name, e in sorted(manifest["cases"].items()):
         data = golden_input(name)
