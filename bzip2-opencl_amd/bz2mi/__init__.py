@@ -16,7 +16,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbz2mi.so")
+# BZ2MI_LIBRARY: an alternative build of the library (A/B experiments)
+LIB_PATH = os.environ.get("BZ2MI_LIBRARY") or os.path.join(_HERE, "libbz2mi.so")
 
 BZ2MI_OK = 0
 BZ2MI_EINVAL = -1

@@ -81,6 +81,18 @@ struct bz2mi_ctx {
     size_t out_words = 0;
     uint8_t* d_scratch = nullptr;
     uint32_t* d_counter = nullptr;
+    // BWT split (bwt.hip): per-block SA, bucket queue, per-block group lists
+    uint32_t* d_sa = nullptr;
+    uint64_t* d_bq = nullptr;
+    uint32_t* d_bcnt = nullptr;  // [0] queued buckets, [1] blocks with large buckets, [2] blocks with
+                                 // groups, [3] [4] pull counters of the large / doubling kernels
+    bz2mi::BwtSeg* d_large = nullptr;
+    uint32_t* d_nlarge = nullptr;
+    uint32_t* d_ngroups = nullptr;
+    uint32_t* d_clist = nullptr;
+    uint32_t* d_p2list = nullptr;
+    bz2mi::BwtSeg* d_groups = nullptr;
+    int cus = 256;
     uint32_t* d_crctab = nullptr;
     // front-end buffers (device RLE1 path)
     size_t fe_n = 0;
@@ -141,6 +153,14 @@ int ensure_capacity(bz2mi_ctx* c, int nblocks) {
     if ((r = dalloc(&c->d_crc, B))) return r;
     if ((r = dalloc(&c->d_bwt, B * c->stride))) return r;
     if ((r = dalloc(&c->d_orig, B))) return r;
+    if ((r = dalloc(&c->d_sa, B * c->stride))) return r;
+    if ((r = dalloc(&c->d_bq, B * 256))) return r;
+    if ((r = dalloc(&c->d_large, B * 256))) return r;
+    if ((r = dalloc(&c->d_nlarge, B))) return r;
+    if ((r = dalloc(&c->d_ngroups, B))) return r;
+    if ((r = dalloc(&c->d_clist, B))) return r;
+    if ((r = dalloc(&c->d_p2list, B))) return r;
+    if ((r = dalloc(&c->d_groups, B * bz2mi::bwt_group_stride(c->stride)))) return r;
     if ((r = dalloc(&c->d_ranks, B * c->stride))) return r;
     if ((r = dalloc(&c->d_rec, B * 64 * 512))) return r;
     if ((r = dalloc(&c->d_mtf, B * c->mtf_stride))) return r;
@@ -165,10 +185,27 @@ int run_blocks(bz2mi_ctx* c, int nb) {
     hipStream_t s = c->stream;
     (void)hipGetLastError();
     HIPCHECK(hipEventRecord(c->ev[0], s));
-    HIPCHECK(hipMemsetAsync(c->d_counter, 0, sizeof(uint32_t), s));
-    const int grid_bwt = std::min(nb, c->bwt_slots);
-    hipLaunchKernelGGL(bwt_kernel, dim3(grid_bwt), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens, nb,
-                       c->d_bwt, c->d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, c->d_counter);
+    HIPCHECK(hipMemsetAsync(c->d_bcnt, 0, 8 * sizeof(uint32_t), s));
+    const int slots = std::min(nb, c->bwt_slots);
+    hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens, nb, c->d_sa,
+                       c->d_bwt, c->d_orig, c->d_bq, c->d_bcnt, c->d_large, c->d_nlarge, c->d_ngroups, c->d_clist,
+                       c->d_bcnt + 1);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("bwt_bucket");
+    hipLaunchKernelGGL(bwt_small_kernel, dim3(c->cus * 8), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens,
+                       c->d_sa, c->d_bwt, c->d_orig, c->d_bq, c->d_bcnt, c->d_groups, c->d_ngroups, c->d_p2list,
+                       c->d_bcnt + 2);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("bwt_small");
+    hipLaunchKernelGGL(bwt_large_kernel, dim3(slots), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens, nb,
+                       c->d_sa, c->d_bwt, c->d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, c->d_large,
+                       c->d_nlarge, c->d_groups, c->d_ngroups, c->d_p2list, c->d_bcnt + 2, c->d_clist,
+                       c->d_bcnt + 1, c->d_bcnt + 3);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("bwt_large");
+    hipLaunchKernelGGL(bwt_double_kernel, dim3(slots), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens, nb,
+                       c->d_sa, c->d_bwt, c->d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, c->d_groups,
+                       c->d_ngroups, c->d_p2list, c->d_bcnt + 2, c->d_bcnt + 4);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt");
     HIPCHECK(hipEventRecord(c->ev[1], s));
@@ -453,8 +490,10 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     hipDeviceProp_t prop;
     int cus = 256;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+    c->cus = cus;
     c->bwt_slots = cus * 4;
     if (dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S)) || dalloc(&c->d_counter, 4) ||
+        dalloc(&c->d_bcnt, 8) ||
         dalloc(&c->d_state, (size_t)c->p * bz2mi::kMaxAlpha)) {
         bz2mi_destroy(c);
         return nullptr;
@@ -477,7 +516,9 @@ void bz2mi_destroy(bz2mi_ctx* c) {
     void* ptrs[] = {c->d_blocks, c->d_lens, c->d_crc, c->d_bwt, c->d_orig, c->d_ranks, c->d_rec, c->d_mtf,
                     c->d_mtflen, c->d_alpha, c->d_hist, c->d_present, c->d_seed, c->d_state, c->d_payload,
                     c->d_pbits, c->d_offs, c->d_out, c->d_scratch, c->d_counter, c->d_crctab, c->d_in,
-                    c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd, c->d_starts, c->d_nb};
+                    c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd, c->d_starts, c->d_nb,
+                    c->d_sa, c->d_bq, c->d_bcnt, c->d_large, c->d_nlarge, c->d_ngroups, c->d_clist, c->d_p2list,
+                    c->d_groups};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)

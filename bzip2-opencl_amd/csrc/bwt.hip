@@ -59,9 +59,7 @@ struct BwtShared {
     uint32_t bcast[4];
 };
 
-struct Seg {
-    uint32_t start, len;
-};
+using Seg = BwtSeg;
 
 struct Scratch {
     uint32_t* sa;
@@ -120,139 +118,180 @@ __device__ __forceinline__ uint8_t byte_at(const uint8_t* __restrict__ T, int n,
     return T[pos >= (uint32_t)n ? pos % (uint32_t)n : pos];
 }
 
-// ---- wave-level register bitonic sort of 64*E (key, index) pairs, striped
-// (element e of lane l is item e*64 + l); ascending by (hi, lo).
-template <int E>
-__device__ __forceinline__ void wave_bitonic(uint64_t (&hi)[E], uint32_t (&lo)[E]) {
+// ---- wave-level register bitonic sort of 64*E items, blocked (item l*E+e
+// sits in element e of lane l): partners closer than E are in the same lane,
+// farther ones are lane ^ (j/E) reached with DPP / permlane moves.
+// WITH_LO: a 32-bit payload travels with each 64-bit key (not compared).
+template <int E, bool WITH_LO, int K, int J>
+__device__ __forceinline__ void bitonic_stage(uint64_t (&key)[E], uint32_t (&lo)[E]) {
     const int lane = lane_id();
+    if constexpr (J < E) {
 #pragma unroll
-    for (int k = 2; k <= 64 * E; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j >= 1; j >>= 1) {
-            if (j >= 64) {
-                const int je = j / 64;
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const int pe = e ^ je;
-                    if (pe > e) {
-                        const bool asc = (((e * 64) & k) == 0);  // k >= 128 here: lane bits do not matter
-                        const bool gt = hi[e] > hi[pe] || (hi[e] == hi[pe] && lo[e] > lo[pe]);
-                        if (gt == asc) {
-                            const uint64_t th = hi[e];
-                            hi[e] = hi[pe];
-                            hi[pe] = th;
-                            const uint32_t tl = lo[e];
-                            lo[e] = lo[pe];
-                            lo[pe] = tl;
-                        }
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const uint64_t oh = __shfl_xor(hi[e], j);
-                    const uint32_t ol = __shfl_xor(lo[e], j);
-                    const int g = e * 64 + lane;
-                    const bool asc = (g & k) == 0;
-                    const bool lower = (lane & j) == 0;
-                    const bool mine_gt = hi[e] > oh || (hi[e] == oh && lo[e] > ol);
-                    // lower slot keeps the min when ascending, the max when descending
-                    const bool take = (lower == asc) ? mine_gt : !mine_gt;
-                    if (take) {
-                        hi[e] = oh;
-                        lo[e] = ol;
+        for (int e = 0; e < E; ++e) {
+            const int pe = e ^ J;
+            if (pe > e) {
+                const bool asc = ((lane * E + e) & K) == 0;
+                if ((key[e] > key[pe]) == asc) {
+                    const uint64_t tk = key[e];
+                    key[e] = key[pe];
+                    key[pe] = tk;
+                    if (WITH_LO) {
+                        const uint32_t tl = lo[e];
+                        lo[e] = lo[pe];
+                        lo[pe] = tl;
                     }
                 }
             }
+
+        }
+    } else {
+        constexpr int LJ = J / E;
+        const bool lower = (lane & LJ) == 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint64_t ok = ((uint64_t)xor_lanes<LJ>((uint32_t)(key[e] >> 32)) << 32) |
+                                xor_lanes<LJ>((uint32_t)key[e]);
+            const uint32_t ol = WITH_LO ? xor_lanes<LJ>(lo[e]) : 0u;
+            const bool asc = ((lane * E + e) & K) == 0;
+            // lower slot keeps the min when ascending, the max when descending
+            // (on equal keys a swap of payloads is harmless: ties do not matter
+            // in mode 0 and keys are unique in mode 1)
+            const bool take = (ok < key[e]) == (lower == asc);
+            if (take) {
+                key[e] = ok;
+                if (WITH_LO) lo[e] = ol;
+            }
+
         }
     }
 }
 
-// Sort one small segment with one wave, relabel its members and emit its
-// groups of size > 1 to `out` (slot from *counter).
-// mode 0: keys are the 8 bytes at depth d (phase 1); mode 1: keys from ka[] (phase 2).
-template <int E>
-__device__ void wave_sort_segment(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d, int mode,
-                                  Seg* out, uint32_t* counter) {
+template <int E, bool WITH_LO, int K, int J>
+__device__ __forceinline__ void bitonic_merge(uint64_t (&key)[E], uint32_t (&lo)[E]) {
+    bitonic_stage<E, WITH_LO, K, J>(key, lo);
+    if constexpr (J > 1) bitonic_merge<E, WITH_LO, K, J / 2>(key, lo);
+}
+
+template <int E, bool WITH_LO, int K>
+__device__ __forceinline__ void bitonic_from(uint64_t (&key)[E], uint32_t (&lo)[E]) {
+    bitonic_merge<E, WITH_LO, K, K / 2>(key, lo);
+    if constexpr (K < 64 * E) bitonic_from<E, WITH_LO, K * 2>(key, lo);
+}
+
+// every stage is a compile-time (K, J) pair, so all indices are constants
+template <int E, bool WITH_LO>
+__device__ __forceinline__ void wave_bitonic(uint64_t (&key)[E], uint32_t (&lo)[E]) {
+    bitonic_from<E, WITH_LO, 2>(key, lo);
+}
+
+// Where a sort puts the groups (equal keys, size > 1) it leaves behind: a list
+// with a capacity; the first group of a block can also enlist the block for
+// the phase-2 kernel.
+struct GroupSink {
+    Seg* out;
+    uint32_t* counter;
+    uint32_t cap;
+    uint32_t* worklist;  // nullptr inside the per-block kernel
+    uint32_t* wcount;
+    uint32_t block;
+
+    __device__ __forceinline__ void push(Seg g) const {
+        const uint32_t slot = atomicAdd(counter, 1u);
+        if (slot < cap) out[slot] = g;
+        if (worklist && slot == 0) worklist[atomicAdd(wcount, 1u)] = block;
+    }
+};
+
+__device__ __forceinline__ GroupSink local_sink(Seg* out, uint32_t* counter) {
+    return GroupSink{out, counter, 0xffffffffu, nullptr, nullptr, 0};
+}
+
+__device__ __forceinline__ uint8_t bwt_byte(const uint8_t* __restrict__ T, int n, uint32_t i) {
+    return T[i == 0 ? (uint32_t)n - 1 : i - 1];
+}
+
+// Sort one small segment with one wave and emit its groups of size > 1 to
+// `out` (slot from *counter).
+// mode 0 (phase 1): keys = the 8 bytes at depth d, rotation index carried
+//   alongside; ties do not matter (equal keys become a group).  Sorted
+//   positions get their BWT byte (and origPtr) directly; labels are deferred.
+// mode 1 (phase 2): keys = (snapshot label << 20) | index from ka[]; members
+//   get their new labels.
+template <int E, int MODE>
+__device__ void wave_sort_segment(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
+                                  const GroupSink& sink, uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig) {
     const int lane = lane_id();
-    uint64_t hi[E];
+    uint64_t key[E];
     uint32_t lo[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        const uint32_t g = (uint32_t)(e * 64 + lane);
+        const uint32_t g = (uint32_t)(lane * E + e);
         if (g < seg.len) {
-            const uint32_t i = s.sa[seg.start + g];
-            lo[e] = i;
-            if (mode == 0) {
+            if (MODE == 0) {
+                // payload: rotation index, its BWT byte T[i-1] in bits 24..31
+                const uint32_t i = s.sa[seg.start + g];
                 uint32_t p = i + d;
                 if (p >= (uint32_t)n) p %= (uint32_t)n;
-                hi[e] = load8(T, n, p);
+                key[e] = load8(T, n, p);
+                lo[e] = i | ((uint32_t)bwt_byte(T, n, i) << 24);
             } else {
-                hi[e] = s.ka[seg.start + g];
+                key[e] = s.ka[seg.start + g];
+                lo[e] = 0;
             }
         } else {
-            hi[e] = ~0ull;
+            key[e] = ~0ull;
             lo[e] = ~0u;
         }
     }
-    wave_bitonic<E>(hi, lo);
-    // group boundaries (by key only) and group-start labels
+    wave_bitonic<E, MODE == 0>(key, lo);
+    constexpr int kShift = MODE == 0 ? 0 : kIdxBits;
+    // group flags (key part only), group starts by a max-scan, group ends by
+    // "the next item starts a group"
+    const uint64_t last_key = key[E - 1] >> kShift;
+    const uint64_t prev_last = ((uint64_t)lane_prev((uint32_t)(last_key >> 32)) << 32) | lane_prev((uint32_t)last_key);
     bool flag[E];
-    uint32_t gs[E];
-    uint32_t carry = 0;
+    uint32_t gsl[E];
+    uint32_t run = 0, lmax = 0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        const uint32_t g = (uint32_t)(e * 64 + lane);
-        uint64_t ph = __shfl_up(hi[e], 1);
-        if (e > 0) {
-            const uint64_t last_prev = __shfl(hi[e > 0 ? e - 1 : 0], 63);
-            if (lane == 0) ph = last_prev;
-        }
-        flag[e] = (g == 0) || (hi[e] != ph);
-        uint32_t v = flag[e] ? g : 0u;
-        v = wave_incl_max(v);
-        v = v > carry ? v : carry;
-        gs[e] = v;
-        carry = __shfl(v, 63);
-        if (g < seg.len) s.sa[seg.start + g] = lo[e];
+        const uint32_t g = (uint32_t)(lane * E + e);
+        const uint64_t pk = e ? key[e - 1] >> kShift : prev_last;
+        flag[e] = g == 0 || (key[e] >> kShift) != pk;
+        if (flag[e] && g < seg.len) run = g;
+        gsl[e] = run;
+        lmax = run;
     }
-    // end of each group = the next flag position (suffix min), or len
-    uint32_t ncarry = seg.len;
+    const uint32_t before = lane_prev(wave_incl_max(lmax), 0u);
+    const bool next_lane_flag = __shfl_down((int)flag[0], 1) != 0;  // (lane 63: unused)
 #pragma unroll
-    for (int e = E - 1; e >= 0; --e) {
-        const uint32_t g = (uint32_t)(e * 64 + lane);
-        uint32_t v = (flag[e] && g < seg.len) ? g : seg.len;
-        for (int dd = 1; dd < 64; dd <<= 1) {  // inclusive suffix min
-            const uint32_t y = __shfl_down(v, dd);
-            if (lane + dd < 64) v = v < y ? v : y;
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(lane * E + e);
+        if (g >= seg.len) continue;
+        const uint32_t i = MODE == 0 ? lo[e] & 0xffffffu : (uint32_t)(key[e] & ((1u << kIdxBits) - 1u));
+        const uint32_t gs = gsl[e] > before ? gsl[e] : before;
+        s.sa[seg.start + g] = i;
+        if (MODE == 0) {
+            bwt[seg.start + g] = (uint8_t)(lo[e] >> 24);
+            if (i == 0) *orig = seg.start + g;
+        } else {
+            s.rank[i] = seg.start + gs;
         }
-        uint32_t after = __shfl_down(v, 1);
-        if (lane == 63) after = ncarry;
-        after = after < ncarry ? after : ncarry;
-        const uint32_t first_here = __shfl(v, 0);
-        if (g < seg.len) {
-            s.rank[lo[e]] = seg.start + gs[e];
-            if (flag[e]) {
-                const uint32_t glen = after - g;
-                if (glen > 1) {
-                    const uint32_t slot = atomicAdd(counter, 1u);
-                    out[slot] = Seg{seg.start + g, glen};
-                }
-            }
-        }
-        ncarry = first_here < ncarry ? first_here : ncarry;
+        const bool nf = e + 1 < E ? flag[e + 1 < E ? e + 1 : 0] : next_lane_flag;
+        if ((g + 1 == seg.len || nf) && g > gs) sink.push(Seg{seg.start + gs, g - gs + 1});
     }
 }
 
+// (see GroupSink)
 // dispatch a small segment to the right register width
-__device__ void wave_sort_any(const uint8_t* T, int n, Scratch& s, Seg seg, uint32_t d, int mode, Seg* out,
-                              uint32_t* counter) {
+template <int MODE>
+__device__ void wave_sort_any(const uint8_t* T, int n, Scratch& s, Seg seg, uint32_t d, const GroupSink& sink,
+                              uint8_t* bwt, uint32_t* orig) {
     seg.start = uniform(seg.start);
     seg.len = uniform(seg.len);
-    if (seg.len <= 64) wave_sort_segment<1>(T, n, s, seg, d, mode, out, counter);
-    else if (seg.len <= 128) wave_sort_segment<2>(T, n, s, seg, d, mode, out, counter);
-    else if (seg.len <= 256) wave_sort_segment<4>(T, n, s, seg, d, mode, out, counter);
-    else wave_sort_segment<8>(T, n, s, seg, d, mode, out, counter);
+    if (seg.len <= 64) wave_sort_segment<1, MODE>(T, n, s, seg, d, sink, bwt, orig);
+    else if (seg.len <= 128) wave_sort_segment<2, MODE>(T, n, s, seg, d, sink, bwt, orig);
+    else if (seg.len <= 256) wave_sort_segment<4, MODE>(T, n, s, seg, d, sink, bwt, orig);
+    else wave_sort_segment<8, MODE>(T, n, s, seg, d, sink, bwt, orig);
 }
 
 // ---- workgroup LSD radix (large phase-2 groups)
@@ -346,7 +385,7 @@ __device__ void wg_sort_group(Scratch& s, Seg seg, BwtShared& sh, Seg* out, uint
     uint32_t* v1 = s.vb + seg.start;
     for (int k = t; k < m; k += NT) {
         const uint32_t i = s.sa[seg.start + k];
-        k0[k] = (k0[k] << kIdxBits) | i;  // composite (key, index)
+        (void)k0;  // keys were snapshotted as (label << 20) | index
         v0[k] = i;
     }
     __syncthreads();
@@ -395,7 +434,8 @@ __device__ void wg_sort_group(Scratch& s, Seg seg, BwtShared& sh, Seg* out, uint
 // Phase 1 large bucket at depth d: partition by byte d; children go to the
 // small list, the next large list, or are finished (size 1 / depth limit).
 __device__ void wg_partition(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d, BwtShared& sh,
-                             Seg* large_next) {
+                             Seg* large_next, const GroupSink& sink, uint8_t* __restrict__ bwt,
+                             uint32_t* __restrict__ orig) {
     seg.start = uniform(seg.start);
     seg.len = uniform(seg.len);
     const int t = threadIdx.x;
@@ -421,14 +461,15 @@ __device__ void wg_partition(const uint8_t* __restrict__ T, int n, Scratch& s, S
     __syncthreads();
     // children: bucket t spans [ex, ex + c)
     if (c == 1) {
-        s.rank[s.sa[seg.start + ex]] = seg.start + ex;
+        const uint32_t i = s.sa[seg.start + ex];
+        bwt[seg.start + ex] = bwt_byte(T, n, i);
+        if (i == 0) *orig = seg.start + ex;
     } else if (c > 1) {
         const Seg ch{seg.start + ex, c};
         if (c <= (uint32_t)kSmall) {
             s.small[atomicAdd(&sh.cnt[0], 1u)] = ch;
         } else if (d + 1 >= (uint32_t)kMaxDepth) {
-            for (uint32_t k = 0; k < c; ++k) s.rank[s.sa[ch.start + k]] = ch.start;
-            s.grp[atomicAdd(&sh.cnt[2], 1u)] = ch;
+            sink.push(ch);
         } else {
             large_next[atomicAdd(&sh.cnt[3], 1u)] = ch;
         }
@@ -436,32 +477,49 @@ __device__ void wg_partition(const uint8_t* __restrict__ T, int n, Scratch& s, S
     __syncthreads();
 }
 
-__device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restrict__ out, uint32_t* __restrict__ orig,
-                          Scratch& s, BwtShared& sh, bool stamp) {
+// ---- phase 1a: counting sort of the rotations by their first byte into sa.
+// Thread t gets bucket t: start *ex, size *c.
+__device__ void count_sort_first(const uint8_t* __restrict__ T, int n, uint32_t* __restrict__ sa, BwtShared& sh,
+                                 uint32_t* c_out, uint32_t* ex_out) {
     const int t = threadIdx.x;
-    BZ2MI_PHASE(g_bwt_phase, 0, stamp);
-    // ---- phase 1a: counting sort by the first byte
     sh.hist[t] = 0;
-    if (t < 8) sh.cnt[t] = 0;
     __syncthreads();
-    for (int i = t; i < n; i += NT) atomicAdd(&sh.hist[T[i]], 1u);
-    __syncthreads();
-    {
-        const uint32_t c = sh.hist[t];
-        uint32_t total;
-        const uint32_t ex = wg_excl_sum<NT>(c, sh.tmp, &total);
-        sh.base[t] = ex;
-        __syncthreads();
-        for (int i = t; i < n; i += NT) s.sa[atomicAdd(&sh.base[T[i]], 1u)] = (uint32_t)i;
-        __syncthreads();
-        if (c == 1) s.rank[s.sa[ex]] = ex;
-        else if (c > 1) {
-            if (c <= (uint32_t)kSmall) s.small[atomicAdd(&sh.cnt[0], 1u)] = Seg{ex, c};
-            else s.large[atomicAdd(&sh.cnt[1], 1u)] = Seg{ex, c};
-        }
-        __syncthreads();
+    // 16 bytes per thread and step (blocks are 64-byte aligned)
+    const int n16 = n >> 4;
+    const uint4* T4 = reinterpret_cast<const uint4*>(T);
+    for (int v = t; v < n16; v += NT) {
+        const uint4 w = T4[v];
+        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) atomicAdd(&sh.hist[(ww[k >> 2] >> ((k & 3) * 8)) & 255u], 1u);
     }
-    BZ2MI_PHASE(g_bwt_phase, 1, stamp);
+    for (int i = (n16 << 4) + t; i < n; i += NT) atomicAdd(&sh.hist[T[i]], 1u);
+    __syncthreads();
+    const uint32_t c = sh.hist[t];
+    uint32_t total;
+    const uint32_t ex = wg_excl_sum<NT>(c, sh.tmp, &total);
+    sh.base[t] = ex;
+    __syncthreads();
+    for (int v = t; v < n16; v += NT) {
+        const uint4 w = T4[v];
+        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            sa[atomicAdd(&sh.base[(ww[k >> 2] >> ((k & 3) * 8)) & 255u], 1u)] = (uint32_t)(v * 16 + k);
+    }
+    for (int i = (n16 << 4) + t; i < n; i += NT) sa[atomicAdd(&sh.base[T[i]], 1u)] = (uint32_t)i;
+    __syncthreads();
+    *c_out = c;
+    *ex_out = ex;
+}
+
+// ---- phase 1b: expects the small / large bucket lists (sh.cnt[0], [1])
+// (expects the large list in s.large, count sh.cnt[1], no small buckets yet;
+// groups go to `sink`)
+__device__ void bwt_levels(const uint8_t* __restrict__ T, int n, uint8_t* __restrict__ out,
+                           uint32_t* __restrict__ orig, Scratch& s, BwtShared& sh, const GroupSink& sink,
+                           bool stamp) {
+    const int t = threadIdx.x;
     // ---- phase 1b: levels of (small sorts, large partitions)
     uint32_t depth = 1;
     Seg* large = s.large;
@@ -476,7 +534,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
             if (lane_id() == 0) idx = atomicAdd(&sh.cnt[4], 1u);
             idx = uniform(__shfl(idx, 0));
             if (idx >= nsmall) break;
-            wave_sort_any(T, n, s, s.small[idx], depth, 0, s.grp, &sh.cnt[2]);
+            wave_sort_any<0>(T, n, s, s.small[idx], depth, sink, out, orig);
         }
         __syncthreads();
         BZ2MI_PHASE(g_bwt_phase, 2, stamp && depth == 1);
@@ -487,7 +545,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
             sh.cnt[3] = 0;
         }
         __syncthreads();
-        for (uint32_t q = 0; q < nlarge; ++q) wg_partition(T, n, s, large[q], depth, sh, large_next);
+        for (uint32_t q = 0; q < nlarge; ++q) wg_partition(T, n, s, large[q], depth, sh, large_next, sink, out, orig);
         if (t == 0) sh.cnt[1] = sh.cnt[3];
         __syncthreads();
         Seg* tmpl = large;
@@ -496,10 +554,35 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
         depth++;
     }
     BZ2MI_PHASE(g_bwt_phase, 3, stamp);
+}
+
+// ---- labels, phase 2 and the reordered BWT bytes: expects the groups left
+// by phase 1 in s.grp (count sh.cnt[2])
+__device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __restrict__ out,
+                           uint32_t* __restrict__ orig, Scratch& s, BwtShared& sh, bool stamp) {
+    const int t = threadIdx.x;
+    // ---- labels for phase 2 (only when groups are left): every position is
+    // its own label, members of a group carry the group's start
+    uint32_t ng = uniform(sh.cnt[2]);
+    if (ng > 0) {
+        for (int k = t; k < n; k += NT) s.rank[s.sa[k]] = (uint32_t)k;
+        __syncthreads();
+        if (t == 0) sh.cnt[4] = 0;
+        __syncthreads();
+        for (;;) {
+            uint32_t idx = 0;
+            if (lane_id() == 0) idx = atomicAdd(&sh.cnt[4], 1u);
+            idx = uniform(__shfl(idx, 0));
+            if (idx >= ng) break;
+            const Seg sg = s.grp[idx];
+            for (uint32_t k = lane_id(); k < sg.len; k += 64) s.rank[s.sa[sg.start + k]] = sg.start;
+        }
+        __syncthreads();
+    }
     // ---- phase 2: prefix doubling on the unresolved groups
     Seg* g = s.grp;
     Seg* g2 = s.grp2;
-    uint32_t ng = uniform(sh.cnt[2]);
+    const bool doubled = ng > 0;
     for (long long h = 9; ng > 0 && h < n; h <<= 1) {
         // pass A: snapshot keys label[i+h] for every member of every group
         if (t == 0) sh.cnt[4] = 0;
@@ -513,7 +596,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
             for (uint32_t k = lane_id(); k < sg.len; k += 64) {
                 const uint32_t i = s.sa[sg.start + k];
                 const uint32_t ih = (uint32_t)((i + h) % n);
-                s.ka[sg.start + k] = s.rank[ih];
+                s.ka[sg.start + k] = ((uint64_t)s.rank[ih] << kIdxBits) | i;
             }
         }
         __syncthreads();
@@ -534,7 +617,7 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
             idx = uniform(__shfl(idx, 0));
             if (idx >= ng) break;
             const Seg sg = g[idx];
-            if (sg.len <= (uint32_t)kSmall) wave_sort_any(T, n, s, sg, 0, 1, g2, &sh.cnt[5]);
+            if (sg.len <= (uint32_t)kSmall) wave_sort_any<1>(T, n, s, sg, 0, local_sink(g2, &sh.cnt[5]), out, orig);
         }
         __syncthreads();
         ng = uniform(sh.cnt[5]);
@@ -544,43 +627,181 @@ __device__ void bwt_block(const uint8_t* __restrict__ T, int n, uint8_t* __restr
         __syncthreads();
     }
     BZ2MI_PHASE(g_bwt_phase, 4, stamp);
-    // ---- BWT bytes and origPtr
-    for (int k = t; k < n; k += NT) {
-        const uint32_t i = s.sa[k];
-        out[k] = T[i == 0 ? n - 1 : i - 1];
-        if (i == 0) *orig = (uint32_t)k;
+    // ---- BWT bytes and origPtr of the positions phase 2 reordered (phase 1
+    // wrote the others as it placed them); 4 positions per thread and step
+    if (doubled) {
+        const int n4 = n >> 2;
+        const uint4* SA4 = reinterpret_cast<const uint4*>(s.sa);
+        uint32_t* O4 = reinterpret_cast<uint32_t*>(out);
+        for (int v = t; v < n4; v += NT) {
+            const uint4 q = SA4[v];
+            const uint32_t ii[4] = {q.x, q.y, q.z, q.w};
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                w |= (uint32_t)bwt_byte(T, n, ii[k]) << (8 * k);
+                if (ii[k] == 0) *orig = (uint32_t)(v * 4 + k);
+            }
+            O4[v] = w;
+        }
+        for (int k = (n4 << 2) + t; k < n; k += NT) {
+            const uint32_t i = s.sa[k];
+            out[k] = bwt_byte(T, n, i);
+            if (i == 0) *orig = (uint32_t)k;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     BZ2MI_PHASE(g_bwt_phase, 5, stamp);
 }
 
+constexpr int kQLenBits = 10, kQStartBits = 20;
+
+
 }  // namespace
 
-__global__ __launch_bounds__(256) void bwt_kernel(const uint8_t* __restrict__ blocks, size_t stride,
-                                                  const uint32_t* __restrict__ lens, int nblocks,
-                                                  uint8_t* __restrict__ bwt_out, uint32_t* __restrict__ orig_out,
-                                                  uint8_t* scratch, size_t scratch_per_slot, int S,
-                                                  uint32_t* work_counter) {
+// ---- kernel 1: per block, counting sort of the rotations by their first
+// byte.  Buckets of <= 512 go to the queue of kernel 2 (all blocks), larger
+// ones to the block's large list for kernel 3.
+__global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                         const uint32_t* __restrict__ lens, int nblocks,
+                                                         uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                         uint32_t* __restrict__ orig_out, uint64_t* __restrict__ queue,
+                                                         uint32_t* __restrict__ qcount, Seg* __restrict__ large_all,
+                                                         uint32_t* __restrict__ nlarge, uint32_t* __restrict__ ngroups,
+                                                         uint32_t* __restrict__ clist, uint32_t* __restrict__ ccount) {
+    __shared__ BwtShared sh;
+    const int b = blockIdx.x;
+    if (b >= nblocks) return;
+    const int t = threadIdx.x;
+    const int n = (int)uniform(lens[b]);
+    const uint8_t* T = blocks + (size_t)b * stride;
+    uint8_t* out = bwt_out + (size_t)b * stride;
+    if (t == 0) ngroups[b] = 0;
+    if (n <= 1) {
+        if (t == 0) {
+            if (n == 1) out[0] = T[0];
+            orig_out[b] = 0;
+            nlarge[b] = 0;
+        }
+        return;
+    }
+    uint32_t* sa = sa_all + (size_t)b * stride;
+    uint32_t c, ex;
+    count_sort_first(T, n, sa, sh, &c, &ex);
+    if (c == 1) {
+        const uint32_t i = sa[ex];
+        out[ex] = bwt_byte(T, n, i);
+        if (i == 0) orig_out[b] = ex;
+    }
+    const bool small = c > 1 && c <= (uint32_t)kSmall, large = c > (uint32_t)kSmall;
+    uint32_t nq, nl;
+    const uint32_t r = wg_excl_sum<NT>(small ? 1u : 0u, sh.tmp, &nq);
+    const uint32_t rl = wg_excl_sum<NT>(large ? 1u : 0u, sh.tmp, &nl);
+    if (t == 0) {
+        sh.bcast[0] = nq ? atomicAdd(qcount, nq) : 0u;
+        nlarge[b] = nl;
+        if (nl) clist[atomicAdd(ccount, 1u)] = (uint32_t)b;
+    }
+    __syncthreads();
+    if (small)
+        queue[sh.bcast[0] + r] = ((uint64_t)b << (kQStartBits + kQLenBits)) | ((uint64_t)ex << kQLenBits) | (c - 1);
+    if (large) large_all[(size_t)b * 256 + rl] = Seg{ex, c};
+}
+
+// ---- kernel 2: one wave per queued bucket (any block): sort by the next 8
+// bytes, write SA, BWT bytes and origPtr; groups go to the block's list
+__global__ __launch_bounds__(256) void bwt_small_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                        const uint32_t* __restrict__ lens,
+                                                        uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                        uint32_t* __restrict__ orig_out,
+                                                        const uint64_t* __restrict__ queue,
+                                                        const uint32_t* __restrict__ qcount, Seg* __restrict__ grp_all,
+                                                        uint32_t* __restrict__ ngroups, uint32_t* __restrict__ p2list,
+                                                        uint32_t* __restrict__ p2count) {
+    const uint32_t nq = uniform(*qcount);
+    const uint32_t nwaves = gridDim.x * (NT / 64);
+    for (uint32_t q = blockIdx.x * (NT / 64) + wave_id(); q < nq; q += nwaves) {
+        const uint64_t e = queue[q];
+        const uint32_t b = uniform((uint32_t)(e >> (kQStartBits + kQLenBits)));
+        const Seg seg{(uint32_t)(e >> kQLenBits) & ((1u << kQStartBits) - 1u),
+                      (uint32_t)(e & ((1u << kQLenBits) - 1u)) + 1u};
+        const int n = (int)uniform(lens[b]);
+        Scratch s{};
+        s.sa = sa_all + (size_t)b * stride;
+        const GroupSink sink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu, p2list, p2count, b};
+        wave_sort_any<0>(blocks + (size_t)b * stride, n, s, seg, 1, sink, bwt_out + (size_t)b * stride,
+                         orig_out + b);
+    }
+}
+
+// ---- kernel 3: blocks with large first-byte buckets, one workgroup slot
+// each (blocks pulled from a counter): levels of partitions by the next byte
+// and wave sorts of the small children
+__global__ __launch_bounds__(256) void bwt_large_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                        const uint32_t* __restrict__ lens, int nblocks,
+                                                        uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                        uint32_t* __restrict__ orig_out, uint8_t* scratch,
+                                                        size_t scratch_per_slot, int S,
+                                                        const Seg* __restrict__ large_all,
+                                                        const uint32_t* __restrict__ nlarge,
+                                                        Seg* __restrict__ grp_all, uint32_t* __restrict__ ngroups,
+                                                        uint32_t* __restrict__ p2list, uint32_t* __restrict__ p2count,
+                                                        const uint32_t* __restrict__ clist,
+                                                        const uint32_t* __restrict__ ccount, uint32_t* pull) {
     __shared__ BwtShared sh;
     Scratch s = carve(scratch + (size_t)blockIdx.x * scratch_per_slot, S);
     const int t = threadIdx.x;
+    const uint32_t nw = uniform(*ccount);
     for (;;) {
-        if (t == 0) sh.bcast[0] = atomicAdd(work_counter, 1u);
+        if (t == 0) sh.bcast[0] = atomicAdd(pull, 1u);
         __syncthreads();
-        // wave-uniform (SGPR) block index and length keep every branch below
-        // uniform; the barrier closing each iteration keeps the back edge
-        // convergent even though lane 0 alone handles tiny blocks
-        const int b = __builtin_amdgcn_readfirstlane((int)sh.bcast[0]);
-        if (b >= nblocks) break;
-        const uint8_t* T = blocks + (size_t)b * stride;
-        uint8_t* out = bwt_out + (size_t)b * stride;
-        const int n = __builtin_amdgcn_readfirstlane((int)lens[b]);
-        if (n > 1) {
-            bwt_block(T, n, out, orig_out + b, s, sh, b == nblocks / 2);
-        } else if (t == 0) {
-            if (n == 1) out[0] = T[0];
-            orig_out[b] = 0;
-        }
+        // wave-uniform (SGPR) values keep every branch below uniform; the
+        // barrier closing each iteration keeps the back edge convergent
+        const uint32_t k = uniform(sh.bcast[0]);
+        if (k >= nw) break;
+        const int b = (int)uniform(clist[k]);
+        const int n = (int)uniform(lens[b]);
+        s.sa = sa_all + (size_t)b * stride;
+        const uint32_t nl = uniform(nlarge[b]);
+        for (uint32_t q = t; q < nl; q += NT) s.large[q] = large_all[(size_t)b * 256 + q];
+        if (t < 8) sh.cnt[t] = 0;
+        if (t == 0) sh.cnt[1] = nl;
+        __syncthreads();
+        const GroupSink sink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu, p2list, p2count,
+                             (uint32_t)b};
+        bwt_levels(blocks + (size_t)b * stride, n, bwt_out + (size_t)b * stride, orig_out + b, s, sh, sink,
+                   b == nblocks / 2);
+        __syncthreads();
+    }
+}
+
+// ---- kernel 4: blocks with groups left: labels, prefix doubling, BWT bytes
+__global__ __launch_bounds__(256) void bwt_double_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                         const uint32_t* __restrict__ lens, int nblocks,
+                                                         uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                         uint32_t* __restrict__ orig_out, uint8_t* scratch,
+                                                         size_t scratch_per_slot, int S, Seg* __restrict__ grp_all,
+                                                         const uint32_t* __restrict__ ngroups,
+                                                         const uint32_t* __restrict__ p2list,
+                                                         const uint32_t* __restrict__ p2count, uint32_t* pull) {
+    __shared__ BwtShared sh;
+    Scratch s = carve(scratch + (size_t)blockIdx.x * scratch_per_slot, S);
+    const int t = threadIdx.x;
+    const uint32_t nw = uniform(*p2count);
+    for (;;) {
+        if (t == 0) sh.bcast[0] = atomicAdd(pull, 1u);
+        __syncthreads();
+        const uint32_t k = uniform(sh.bcast[0]);
+        if (k >= nw) break;
+        const int b = (int)uniform(p2list[k]);
+        const int n = (int)uniform(lens[b]);
+        s.sa = sa_all + (size_t)b * stride;
+        s.grp = grp_all + (size_t)b * bwt_group_stride(stride);
+        if (t < 8) sh.cnt[t] = 0;
+        if (t == 0) sh.cnt[2] = ngroups[b];
+        __syncthreads();
+        bwt_finish(blocks + (size_t)b * stride, n, bwt_out + (size_t)b * stride, orig_out + b, s, sh,
+                   b == nblocks / 2);
         __syncthreads();
     }
 }

@@ -10,9 +10,31 @@ namespace bz2mi {
 // Scratch bytes one BWT workgroup slot needs for blocks of S bytes.
 inline size_t bwt_slot_bytes(int S) { return (size_t)48 * (size_t)S + 4096; }
 
-__global__ void bwt_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
-                           uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,
-                           int S, uint32_t* work_counter);
+// BWT in four launches (bwt.hip): per-block counting sort by the first byte;
+// one wave per small bucket across all blocks; levels of partitions for the
+// blocks with large buckets; prefix doubling for the blocks with groups left.
+struct BwtSeg {
+    uint32_t start, len;
+};
+__global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
+                                  uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint64_t* queue,
+                                  uint32_t* qcount, BwtSeg* large_all, uint32_t* nlarge, uint32_t* ngroups,
+                                  uint32_t* clist, uint32_t* ccount);
+__global__ void bwt_small_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
+                                 uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* queue,
+                                 const uint32_t* qcount, BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list,
+                                 uint32_t* p2count);
+__global__ void bwt_large_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
+                                 uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch,
+                                 size_t scratch_per_slot, int S, const BwtSeg* large_all, const uint32_t* nlarge,
+                                 BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count,
+                                 const uint32_t* clist, const uint32_t* ccount, uint32_t* pull);
+__global__ void bwt_double_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
+                                  uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch,
+                                  size_t scratch_per_slot, int S, BwtSeg* grp_all, const uint32_t* ngroups,
+                                  const uint32_t* p2list, const uint32_t* p2count, uint32_t* pull);
+// per-block group list capacity (BwtSeg entries) for a block stride
+__host__ __device__ inline size_t bwt_group_stride(size_t stride) { return stride / 2 + 2; }
 
 __global__ void mtf_kernel(const uint8_t* bwt, size_t stride, const uint32_t* lens, int nblocks, uint8_t* ranks,
                            uint8_t* rec, uint16_t* mtf_out, size_t mtf_stride, uint32_t* mtf_len,
@@ -21,11 +43,12 @@ __global__ void mtf_kernel(const uint8_t* bwt, size_t stride, const uint32_t* le
 __global__ void seed_kernel(const uint32_t* hist, uint32_t* seed, uint32_t* state, int nblocks, int p,
                             uint64_t first_block);
 
+// phase stamps (make PHASES=1)
 int huffman_phases(unsigned long long* out);
 int bwt_phases(unsigned long long* out);
 int mtf_phases(unsigned long long* out);
 int fe_phases(unsigned long long* out);
-int run_selftest(uint32_t* host_bad, int n);  // cross-lane primitive checks  // phase stamps (make PHASES=1)
+int run_selftest(uint32_t* host_bad, int n);  // cross-lane primitive checks
 __global__ void huffman_kernel(const uint16_t* mtf, size_t mtf_stride, const uint32_t* mtf_len,
                                const uint32_t* alpha_in, const uint32_t* seed, const uint32_t* present,
                                const uint32_t* orig, int nblocks, uint32_t* payload, size_t payload_words,

@@ -21,11 +21,10 @@ for _ in range(2):
 torch.cuda.synchronize()
 L = bz2mi.lib()
 buf = (ctypes.c_ulonglong * 16)()
-for k, name in [(0, "huffman")]:
+for k, name in [(0, "huffman"), (1, "bwt"), (2, "mtf")]:
     r = L.bz2mi_debug_phases(k, buf)
     v = list(buf)
-    print(name, "rc", r, "us:", [round((v[i + 1] - v[i]) / 100.0, 1) if v[i] and v[i + 1] else None for i in range(15) if v[i + 1]],
-          "total", round((max(v) - v[0]) / 100.0, 1))
+    n_ = max(i for i in range(16) if v[i]) if any(v) else 0
+    print(name, "rc", r, "us:", [round((v[i + 1] - v[i]) / 100.0, 1) for i in range(n_) if v[i] and v[i + 1]],
+          "total", round((v[n_] - v[0]) / 100.0, 1) if n_ else None)
 print("timings", ctx.timings())
-if len(v) > 14 and v[13] and v[14]:
-    print("last build_lengths: rank sort", round((v[13] - v[8]) / 100.0, 1), "allocator", round((v[14] - v[13]) / 100.0, 1))
