@@ -361,7 +361,9 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
         if ((r = ensure_capacity(c, (int)std::max<uint64_t>(cnt, 1)))) return r;
         if (cnt) {
             hipLaunchKernelGGL(fe_rle1_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts,
-                               first, cnt, c->d_blocks, c->stride, c->d_lens, c->d_crc, c->d_crctab);
+                               first, cnt, c->d_blocks, c->stride, c->d_lens);
+            hipLaunchKernelGGL(fe_crc_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts,
+                               first, cnt, c->d_crc, c->d_crctab);
             HIPCHECK(hipGetLastError());
             STAGE_DONE("front-rle1");
             if ((r = run_blocks(c, (int)cnt))) return r;

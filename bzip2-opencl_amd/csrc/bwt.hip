@@ -153,10 +153,10 @@ __device__ __forceinline__ void bitonic_stage(uint64_t (&key)[E], uint32_t (&lo)
                                 xor_lanes<LJ>((uint32_t)key[e]);
             const uint32_t ol = WITH_LO ? xor_lanes<LJ>(lo[e]) : 0u;
             const bool asc = ((lane * E + e) & K) == 0;
-            // lower slot keeps the min when ascending, the max when descending
-            // (on equal keys a swap of payloads is harmless: ties do not matter
-            // in mode 0 and keys are unique in mode 1)
-            const bool take = (ok < key[e]) == (lower == asc);
+            // lower slot keeps the min when ascending, the max when descending;
+            // both comparisons strict so that equal keys keep their payloads
+            const bool lt = ok < key[e], gt = key[e] < ok;
+            const bool take = (lower == asc) ? lt : gt;
             if (take) {
                 key[e] = ok;
                 if (WITH_LO) lo[e] = ol;

@@ -25,10 +25,16 @@
 
 namespace bz2mi {
 
-// (the front end is timed per kernel with rocprofv3)
+BZ2MI_PHASE_TABLE(g_fe_phase)
+
+// chain kernel: stamps at the first 16 window starts
 int fe_phases(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fe_phase), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
     (void)out;
     return 0;
+#endif
 }
 
 namespace {
@@ -221,39 +227,77 @@ __global__ __launch_bounds__(256) void fe_cost_kernel(const uint8_t* __restrict_
     if (lane == 0) ccost[c] = sum;
 }
 
-// ---- K5: D map over output positions
+// ---- K5: D map over output positions.  A chunk's entries cover the output
+// range [fc[c], fc[c+1]) exactly once: they are built in LDS by the lanes
+// (64 input bytes each) and written out as one coalesced run.
+constexpr int kDmapMax = CH + CH / 4 + 64;  // RLE1 output of one chunk, at most 5/4 of its bytes
+
 __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
                                                       uint64_t n, uint64_t nc, const uint64_t* __restrict__ fc,
                                                       uint8_t* __restrict__ dmap) {
+    __shared__ uint8_t stage[4][kDmapMax];
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
     if (c >= nc) return;
+    uint8_t* st = stage[wave_id()];
     const int lane = lane_id();
     const uint64_t c0 = c * CH;
     const uint64_t at = c0 + (uint64_t)lane * 64;
-    uint8_t v[64], k[64];
-    load64(x, n, at, v);
-    load64(cost, n, at, k);
+    // 64 input bytes and their costs as 16 dwords each (plus the next byte / cost)
+    uint32_t xv[17], kv[17];
+    if (at + 68 <= n) {
+        const uint4* px = reinterpret_cast<const uint4*>(x + at);
+        const uint4* pk = reinterpret_cast<const uint4*>(cost + at);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 a4 = px[q], b4 = pk[q];
+            xv[4 * q] = a4.x; xv[4 * q + 1] = a4.y; xv[4 * q + 2] = a4.z; xv[4 * q + 3] = a4.w;
+            kv[4 * q] = b4.x; kv[4 * q + 1] = b4.y; kv[4 * q + 2] = b4.z; kv[4 * q + 3] = b4.w;
+        }
+        xv[16] = *reinterpret_cast<const uint32_t*>(x + at + 64);
+        kv[16] = *reinterpret_cast<const uint32_t*>(cost + at + 64);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 17; ++q) {
+            uint32_t a1 = 0, b1 = 0;
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t i = at + 4 * q + r;
+                if (i < n) {
+                    a1 |= (uint32_t)x[i] << (8 * r);
+                    b1 |= (uint32_t)cost[i] << (8 * r);
+                }
+            }
+            xv[q] = a1;
+            kv[q] = b1;
+        }
+    }
     uint32_t lsum = 0;
 #pragma unroll
-    for (int q = 0; q < 64; ++q) lsum += k[q];
-    const uint32_t incl = wave_incl_sum(lsum);
-    uint64_t fg = fc[c] + (incl - lsum);
-    const uint32_t next_v = (at + 64 < n) ? x[at + 64] : 0;
-    const uint32_t next_k = (at + 64 < n) ? cost[at + 64] : 0;
-    for (int q = 0; q < 64; ++q) {
-        const uint64_t i = at + q;
-        const uint32_t ci = k[q];
-        if (ci && i + 2 <= n) {
-            const uint32_t vn = q < 63 ? v[q + 1] : next_v;
-            const uint32_t kn = q < 63 ? k[q + 1] : next_k;
-            const uint32_t rsn = vn != v[q];
-            for (uint32_t r = 0; r < ci; ++r) {
-                const uint32_t d = ci + kn - r;  // Fg(i+2) - y for y = fg + r
-                dmap[fg + r] = (uint8_t)(d | (rsn << 4));
-            }
-        }
-        fg += ci;
+    for (int q = 0; q < 16; ++q) {
+        const uint32_t kw = kv[q];
+        lsum += (kw & 255u) + ((kw >> 8) & 255u) + ((kw >> 16) & 255u) + (kw >> 24);
     }
+    const uint32_t incl = wave_incl_sum(lsum);
+    uint32_t fl = incl - lsum;  // chunk-local output position
+    const uint32_t ctot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    // (entries of the last byte or two of the input stay unwritten: no target
+    // reaches them)
+    const uint64_t lim_i = n >= 2 ? n - 2 : 0;  // bytes i <= n-2 have entries
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        const uint32_t ci = (kv[q >> 2] >> ((q & 3) * 8)) & 255u;
+        const uint32_t vq = (xv[q >> 2] >> ((q & 3) * 8)) & 255u;
+        const uint32_t vn = (xv[(q + 1) >> 2] >> (((q + 1) & 3) * 8)) & 255u;
+        const uint32_t kn = (kv[(q + 1) >> 2] >> (((q + 1) & 3) * 8)) & 255u;
+        const uint32_t hi = (vn != vq) ? 16u : 0u;
+        if (ci && at + q <= lim_i) {
+#pragma unroll
+            for (int r = 0; r < 5; ++r)
+                if (r < (int)ci) st[fl + r] = (uint8_t)(((ci + kn - r) & 15u) | hi);  // Fg(i+2) - y, run-start flag
+        }
+        fl += ci;
+    }
+    uint8_t* dst = dmap + fc[c];
+    for (uint32_t j = lane; j < ctot; j += 64) dst[j] = st[j];
 }
 
 namespace {
@@ -366,19 +410,60 @@ __global__ __launch_bounds__(64) void fe_chain_kernel(const uint8_t* __restrict_
     bool have_y = true;
     uint64_t y = lim;   // block 0 starts at 0 (a run start), Fg(1) = 0
     uint64_t p = 0;
+    // Case-A steps advance y by D + S-6 (D < 16, typically near its running
+    // mean).  One round of loads fetches, for each of the next 64 steps, a
+    // 32-byte window of D bytes around the predicted position (lane m: step
+    // m, 9 aligned dwords); the steps are then followed with readlanes until
+    // one lands outside its window, which starts the next round.
+    uint32_t dsum = 0, dcnt = 0;
+    bool finished = false;
+    int nwin = 0;
     for (;;) {
         if (k + 1 >= max_bnd) break;
         if (have_y) {
             if (y >= ytot) break;  // last block
-            const uint32_t d = dmap[y];
-            if (lane == 0) bnd[k] = y;
-            k++;
-            if (d & 16u) {  // next block starts at a run start
-                y = y + (d & 15u) + lim;
-                continue;
+            BZ2MI_PHASE(g_fe_phase, nwin < 16 ? nwin : 15, nwin < 16);
+            nwin++;
+            const uint64_t ybase = y;
+            const uint32_t dg = dcnt ? dsum / dcnt : 1u;  // predicted mean D
+            // window start of step m: ybase + m (lim + dg) - 16, not before step m's minimum
+            const uint64_t pm = ybase + (uint64_t)lane * (lim + dg);
+            const uint64_t lo_m = ybase + (uint64_t)lane * lim;
+            const uint64_t wstart = pm >= lo_m + 16 ? pm - 16 : lo_m;
+            const uint64_t abase = wstart & ~3ull;
+            uint32_t w[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const uint64_t ad = abase + 4u * q;
+                w[q] = ad + 4 <= ytot ? *reinterpret_cast<const uint32_t*>(dmap + ad) : 0u;
             }
-            p = ginv(f, y);  // next block starts inside a run
-            have_y = false;
+            for (int m = 0; m < 64; ++m) {
+                if (y >= ytot || k + 1 >= max_bnd) {
+                    finished = true;
+                    break;
+                }
+                const uint64_t ws = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)wstart, m) |
+                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wstart >> 32), m) << 32);
+                if (y < ws || y >= ws + 32) break;  // outside the window: new round
+                const uint32_t rel = (uint32_t)(y - (ws & ~3ull));
+                const uint32_t qi = rel >> 2;
+                uint32_t sel = w[0];
+#pragma unroll
+                for (int q = 1; q < 9; ++q) sel = qi == (uint32_t)q ? w[q] : sel;
+                const uint32_t d = ((uint32_t)__builtin_amdgcn_readlane((int)sel, m) >> ((rel & 3u) * 8u)) & 0xffu;
+                if (lane == 0) bnd[k] = y;
+                k++;
+                if (d & 16u) {  // next block starts at a run start
+                    y = y + (d & 15u) + lim;
+                    dsum += d & 15u;
+                    dcnt++;
+                    continue;
+                }
+                p = ginv(f, y);  // next block starts inside a run
+                have_y = false;
+                break;
+            }
+            if (finished) break;
             continue;
         }
         // block starting at p, mid-run: its first run is [p, e)
@@ -453,38 +538,58 @@ __device__ __forceinline__ uint32_t mat_apply(const uint32_t* col, uint32_t v) {
 
 }  // namespace
 
-// ---- K8: RLE1 emission + block CRC, one workgroup per block
+// ---- K8: RLE1 emission, one workgroup per block, tiles of 4096 input bytes:
+// the tile (and the byte before it) is staged in LDS with 16-byte loads,
+// each thread emits its 16 bytes into an LDS copy of the tile's output, which
+// is then written out contiguously.  A count byte that belongs to a piece
+// begun in an earlier tile is written straight to the block.
+constexpr int kTile = 4096;
+constexpr int kTileOut = kTile + kTile / 4 + 16;
+
 __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict__ x, uint64_t n,
                                                       const uint64_t* __restrict__ starts, uint64_t first, uint64_t count,
                                                       uint8_t* __restrict__ blocks, size_t stride,
-                                                      uint32_t* __restrict__ lens, uint32_t* __restrict__ crcs,
-                                                      const uint32_t* __restrict__ crc_table) {
+                                                      uint32_t* __restrict__ lens) {
+    __shared__ uint4 tin4[kTile / 16 + 4];
+    __shared__ uint8_t tout[kTileOut];
     __shared__ uint32_t tmp[8];
-    __shared__ uint32_t tab[256];
-    __shared__ uint32_t colA[8][32];   // A_{L * 2^l}
-    __shared__ uint32_t colT[32];      // A_len
-    __shared__ uint32_t colW[32];
-    __shared__ uint32_t part[256];
     __shared__ uint32_t lastv[256];
     const uint64_t lb = blockIdx.x;  // batch-local block
     if (lb >= count) return;
     const uint64_t b = first + lb;
     const int t = threadIdx.x;
-    tab[t] = crc_table[t];
     const uint64_t p0 = starts[b], p1 = starts[b + 1];
-    const uint64_t len_in = p1 - p0;
     uint8_t* out = blocks + lb * stride;
-    // ---- RLE1 emission, tiles of 256 x 16 bytes
+    const uint8_t* tin = reinterpret_cast<const uint8_t*>(tin4);
     uint32_t o_carry = 0;
     uint64_t rs_carry = p0;  // run start in effect before the tile
-    for (uint64_t base = p0; base < p1; base += 4096) {
+    for (uint64_t base = p0; base < p1; base += kTile) {
+        // stage [abase, abase + 16*nvec) covering base-1 .. base+kTile
+        const uint64_t abase = base ? ((base - 1) & ~15ull) : 0;
+        const uint64_t aend = min(n, base + kTile + 1);
+        const int nvec = (int)((aend - abase + 15) >> 4);
+        for (int v = t; v < nvec; v += 256) {
+            const uint64_t ad = abase + 16ull * (uint64_t)v;
+            if (ad + 16 <= n) {
+                tin4[v] = *reinterpret_cast<const uint4*>(x + ad);
+            } else {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int q = 0; q < 16; ++q)
+                    if (ad + q < n) w[q >> 2] |= (uint32_t)x[ad + q] << ((q & 3) * 8);
+                tin4[v] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+        __syncthreads();
+        const uint32_t off0 = (uint32_t)(base - abase);
         const uint64_t a = base + (uint64_t)t * 16;
         uint8_t v[16];
-        uint32_t prev = (a > 0 && a - 1 < n) ? x[a - 1] : 0;
-        for (int q = 0; q < 16; ++q) v[q] = (a + q < p1) ? x[a + q] : 0;
-        const uint32_t nextb = (a + 16 < p1) ? x[a + 16] : 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = (a + q < p1) ? tin[off0 + t * 16 + q] : 0;
+        const uint32_t prev = a > 0 ? tin[off0 + t * 16 - 1] : 0;
+        const uint32_t nextb = (a + 16 < p1) ? tin[off0 + t * 16 + 16] : 0;
         // last run start (local: i == p0 or x[i] != x[i-1]) inside this thread's bytes
         uint32_t lrs = 0;  // as offset+1 from p0 (0 = none)
+#pragma unroll
         for (int q = 0; q < 16; ++q) {
             const uint64_t i = a + q;
             if (i < p1) {
@@ -497,10 +602,10 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         lastv[t] = mx;
         __syncthreads();
         const uint32_t ex = t ? lastv[t - 1] : 0u;  // exclusive max over earlier threads
-        __syncthreads();
         uint64_t cur = ex ? p0 + ex - 1 : rs_carry;
         // emission counts
         uint32_t e = 0;
+#pragma unroll
         for (int q = 0; q < 16; ++q) {
             const uint64_t i = a + q;
             if (i < p1) {
@@ -512,9 +617,10 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         }
         uint32_t etot;
         const uint32_t eoff = wg_excl_sum<256>(e, tmp, &etot);
-        // write
+        // emit into the LDS copy (o: block-relative output position)
         uint32_t o = o_carry + eoff;
         cur = ex ? p0 + ex - 1 : rs_carry;
+#pragma unroll
         for (int q = 0; q < 16; ++q) {
             const uint64_t i = a + q;
             if (i < p1) {
@@ -524,40 +630,93 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
                 const uint32_t nx = q < 15 ? v[q + 1] : nextb;
                 const bool last = (i + 1 == p1) || nx != v[q] || u == 254;
                 if (u < 3) {
-                    out[o++] = v[q];
+                    tout[o - o_carry] = v[q];
+                    o++;
                 } else if (u == 3) {
-                    out[o] = v[q];
-                    if (last) out[o + 1] = 0;
+                    tout[o - o_carry] = v[q];
+                    if (last) tout[o + 1 - o_carry] = 0;  // else the piece's last byte fills the slot
                     o += 2;
                 } else if (last) {
-                    out[o - 1] = (uint8_t)(u - 3);
+                    if (o - 1 >= o_carry) tout[o - 1 - o_carry] = (uint8_t)(u - 3);
+                    else out[o - 1] = (uint8_t)(u - 3);  // piece begun in an earlier tile
                 }
             }
         }
+        __syncthreads();
+        for (uint32_t j = t; j < etot; j += 256) out[o_carry + j] = tout[j];
         o_carry += etot;
         if (tot) rs_carry = p0 + tot - 1;
         __syncthreads();
     }
     if (t == 0) lens[lb] = o_carry;
-    // ---- block CRC over the input bytes [p0, p1): per-thread crc0 of L bytes
-    // with the range padded at the front by virtual zero bytes (crc0 of
-    // leading zeros is 0), then an ordered tree with A_{L*2^l}.
-    const uint64_t L = (len_in + 255) / 256;
-    const uint64_t pad = L * 256 - len_in;
+}
+
+// ---- K9: block CRC over the input bytes [p0, p1), one workgroup per block.
+// Thread t takes L contiguous bytes (L a multiple of 4, the range padded at
+// the front with virtual zero bytes: crc0 of leading zeros is 0), reads them
+// as aligned dwords and runs a slicing-by-4 CRC; the 256 partial CRCs are then
+// combined by an ordered tree with the maps A_{L*2^l} ("L zero bytes").
+__global__ __launch_bounds__(256) void fe_crc_kernel(const uint8_t* __restrict__ x, uint64_t n,
+                                                     const uint64_t* __restrict__ starts, uint64_t first, uint64_t count,
+                                                     uint32_t* __restrict__ crcs, const uint32_t* __restrict__ crc_table) {
+    __shared__ uint32_t tab[4][256];
+    __shared__ uint32_t colA[8][32];   // A_{L * 2^l}
+    __shared__ uint32_t colT[32];      // A_len
+    __shared__ uint32_t colW[32];
+    __shared__ uint32_t part[256];
+    const uint64_t lb = blockIdx.x;
+    if (lb >= count) return;
+    const uint64_t b = first + lb;
+    const int t = threadIdx.x;
+    tab[0][t] = crc_table[t];
+    __syncthreads();
+    for (int k = 1; k < 4; ++k) {
+        const uint32_t pv = tab[k - 1][t];
+        tab[k][t] = (pv << 8) ^ tab[0][pv >> 24];
+        __syncthreads();
+    }
+    const uint64_t p0 = starts[b], p1 = starts[b + 1];
+    const uint64_t len_in = p1 - p0;
+    const uint64_t L = (((len_in + 255) / 256) + 3) & ~3ull;
+    const int64_t s0 = (int64_t)p1 - 256 * (int64_t)L;  // first (virtual) byte
     uint32_t r = 0;
     {
-        const int64_t s0 = (int64_t)((uint64_t)t * L) - (int64_t)pad;
-        for (uint64_t q = 0; q < L; ++q) {
-            const int64_t j = s0 + (int64_t)q;
-            if (j >= 0) r = (r << 8) ^ tab[((r >> 24) ^ x[p0 + (uint64_t)j]) & 0xffu];
+        const int64_t start = s0 + (int64_t)t * (int64_t)L;
+        const int64_t astart = start >= 0 ? (start & ~3ll) : -((-start + 3) & ~3ll);
+        const uint32_t sh = (uint32_t)(start - astart);  // 0..3
+        auto dword_at = [&](int64_t ad) -> uint32_t {  // little-endian dword of bytes [ad, ad+4), zero outside [p0, p1)
+            if (ad >= (int64_t)p0 && ad + 4 <= (int64_t)p1) return *reinterpret_cast<const uint32_t*>(x + ad);
+            uint32_t w = 0;
+            for (int q = 0; q < 4; ++q) {
+                const int64_t j = ad + q;
+                if (j >= (int64_t)p0 && j < (int64_t)p1) w |= (uint32_t)x[j] << (8 * q);
+            }
+            return w;
+        };
+        uint32_t lo = dword_at(astart);
+        const int nw = (int)(L >> 2);
+        for (int kk = 0; kk < nw; kk += 8) {
+            uint32_t hi[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) hi[q] = kk + q < nw ? dword_at(astart + 4 * (kk + q + 1)) : 0u;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (kk + q < nw) {
+                    const uint32_t wle = sh ? __builtin_amdgcn_alignbyte(hi[q], lo, sh) : lo;
+                    const uint32_t xw = r ^ __builtin_bswap32(wle);
+                    r = tab[3][xw >> 24] ^ tab[2][(xw >> 16) & 255u] ^ tab[1][(xw >> 8) & 255u] ^ tab[0][xw & 255u];
+                    lo = hi[q];
+                }
+            }
         }
     }
     part[t] = r;
+    const uint32_t* ctab = tab[0];
     // A_1 columns, then A_L, A_{2L}, ... by squaring/multiplying (thread k owns column k)
     __syncthreads();
     if (t < 32) {
         const uint32_t e1 = 1u << t;
-        colW[t] = (e1 << 8) ^ tab[e1 >> 24];  // A_1
+        colW[t] = (e1 << 8) ^ ctab[e1 >> 24];  // A_1
     }
     __syncthreads();
     // A_L via binary powering: acc = I
@@ -598,7 +757,7 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
     if (t < 32) {
         colT[t] = 1u << t;
         const uint32_t e1 = 1u << t;
-        colW[t] = (e1 << 8) ^ tab[e1 >> 24];
+        colW[t] = (e1 << 8) ^ ctab[e1 >> 24];
     }
     __syncthreads();
     for (uint64_t e2 = len_in; e2; e2 >>= 1) {

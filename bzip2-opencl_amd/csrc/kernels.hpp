@@ -76,7 +76,8 @@ __global__ void fe_resolve_kernel(const uint8_t* x, const uint8_t* cost, const u
                                   uint64_t n, uint64_t nc, const uint64_t* bnd, const uint64_t* nb_in,
                                   uint64_t* starts);
 __global__ void fe_rle1_kernel(const uint8_t* x, uint64_t n, const uint64_t* starts, uint64_t first, uint64_t count,
-                               uint8_t* blocks, size_t stride, uint32_t* lens, uint32_t* crcs,
-                               const uint32_t* crc_table);
+                               uint8_t* blocks, size_t stride, uint32_t* lens);
+__global__ void fe_crc_kernel(const uint8_t* x, uint64_t n, const uint64_t* starts, uint64_t first, uint64_t count,
+                              uint32_t* crcs, const uint32_t* crc_table);
 
 }  // namespace bz2mi

@@ -21,7 +21,7 @@ for _ in range(2):
 torch.cuda.synchronize()
 L = bz2mi.lib()
 buf = (ctypes.c_ulonglong * 16)()
-for k, name in [(0, "huffman"), (1, "bwt"), (2, "mtf")]:
+for k, name in [(0, "huffman"), (1, "bwt"), (2, "mtf"), (3, "fe_chain windows")]:
     r = L.bz2mi_debug_phases(k, buf)
     v = list(buf)
     n_ = max(i for i in range(16) if v[i]) if any(v) else 0
