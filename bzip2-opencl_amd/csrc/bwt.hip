@@ -654,6 +654,106 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
     BZ2MI_PHASE(g_bwt_phase, 5, stamp);
 }
 
+// ---- a first-byte bucket (<= 512 rotations) on one wave: counting sort by
+// the second byte into sub-buckets, then every rotation of a sub-bucket of
+// <= kSub finds its place by counting the smaller (next 8 bytes, index) pairs
+// of its sub-bucket; larger sub-buckets get the wave bitonic sort at depth 2.
+// For data with a wide alphabet the sub-buckets hold one or two rotations,
+// so this is a few operations per rotation instead of a 512-wide network.
+constexpr int kSub = 32;
+
+struct Bucket2Lds {
+    uint32_t base[257];
+    uint64_t key[kSmall];
+    uint32_t idx[kSmall];  // rotation index | BWT byte << 24
+};
+
+__device__ void wave_sort_bucket2(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, const GroupSink& sink,
+                                  uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig, Bucket2Lds& L) {
+    constexpr int E = kSmall / 64;
+    const int lane = lane_id();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L.base[lane * 4 + j] = 0;
+    uint32_t ii[E], c2[E], slot[E];
+    uint64_t key[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(e * 64 + lane);
+        c2[e] = 0;
+        slot[e] = 0;
+        ii[e] = 0;
+        key[e] = 0;
+        if (g < seg.len) {
+            const uint32_t i = s.sa[seg.start + g];
+            uint32_t p1 = i + 1, p2 = i + 2;
+            if (p1 >= (uint32_t)n) p1 -= (uint32_t)n;
+            if (p2 >= (uint32_t)n) p2 %= (uint32_t)n;
+            c2[e] = T[p1];
+            key[e] = load8(T, n, p2);
+            ii[e] = i | ((uint32_t)bwt_byte(T, n, i) << 24);
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if ((uint32_t)(e * 64 + lane) < seg.len) slot[e] = atomicAdd(&L.base[c2[e]], 1u);
+    // counts -> sub-bucket starts (lane l: counters 4l..4l+3)
+    {
+        const uint32_t h0 = L.base[lane * 4], h1 = L.base[lane * 4 + 1], h2 = L.base[lane * 4 + 2],
+                       h3 = L.base[lane * 4 + 3];
+        const uint32_t sum = h0 + h1 + h2 + h3;
+        const uint32_t ex = wave_incl_sum(sum) - sum;
+        L.base[lane * 4] = ex;
+        L.base[lane * 4 + 1] = ex + h0;
+        L.base[lane * 4 + 2] = ex + h0 + h1;
+        L.base[lane * 4 + 3] = ex + h0 + h1 + h2;
+        if (lane == 0) L.base[256] = seg.len;
+    }
+    uint32_t pos[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        pos[e] = 0;
+        if ((uint32_t)(e * 64 + lane) < seg.len) {
+            pos[e] = L.base[c2[e]] + slot[e];
+            L.key[pos[e]] = key[e];
+            L.idx[pos[e]] = ii[e];
+        }
+    }
+    bool any_big = false;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if ((uint32_t)(e * 64 + lane) >= seg.len) continue;
+        const uint32_t b0 = L.base[c2[e]], m = L.base[c2[e] + 1] - b0;
+        const uint32_t i = ii[e] & 0xffffffu;
+        if (m > (uint32_t)kSub) {  // sorted below as a whole
+            s.sa[seg.start + pos[e]] = i;
+            any_big = true;
+            continue;
+        }
+        uint32_t lt = 0, le = 0, eqlt = 0;
+        for (uint32_t q = 0; q < m; ++q) {
+            const uint64_t kq = L.key[b0 + q];
+            const uint32_t iq = L.idx[b0 + q] & 0xffffffu;
+            lt += kq < key[e];
+            le += kq <= key[e];
+            eqlt += (kq == key[e]) & (iq < i);
+        }
+        const uint32_t fin = seg.start + b0 + lt + eqlt;
+        s.sa[fin] = i;
+        bwt[fin] = (uint8_t)(ii[e] >> 24);
+        if (i == 0) *orig = fin;
+        if (le - lt >= 2 && eqlt == 0) sink.push(Seg{seg.start + b0 + lt, le - lt});
+    }
+    // sub-buckets too large for counting: wave bitonic at depth 2
+    uint64_t bigmask = __ballot(any_big);
+    if (bigmask) {
+        __threadfence_block();  // the SA entries just written are read by other lanes
+        for (int c = 0; c < 256; ++c) {
+            const uint32_t b0 = L.base[c], m = L.base[c + 1] - b0;
+            if (m > (uint32_t)kSub) wave_sort_any<0>(T, n, s, Seg{seg.start + b0, m}, 2, sink, bwt, orig);
+        }
+    }
+}
+
 constexpr int kQLenBits = 10, kQStartBits = 20;
 
 
@@ -718,6 +818,7 @@ __global__ __launch_bounds__(256) void bwt_small_kernel(const uint8_t* __restric
                                                         const uint32_t* __restrict__ qcount, Seg* __restrict__ grp_all,
                                                         uint32_t* __restrict__ ngroups, uint32_t* __restrict__ p2list,
                                                         uint32_t* __restrict__ p2count) {
+    __shared__ Bucket2Lds lds[NT / 64];
     const uint32_t nq = uniform(*qcount);
     const uint32_t nwaves = gridDim.x * (NT / 64);
     for (uint32_t q = blockIdx.x * (NT / 64) + wave_id(); q < nq; q += nwaves) {
@@ -729,8 +830,8 @@ __global__ __launch_bounds__(256) void bwt_small_kernel(const uint8_t* __restric
         Scratch s{};
         s.sa = sa_all + (size_t)b * stride;
         const GroupSink sink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu, p2list, p2count, b};
-        wave_sort_any<0>(blocks + (size_t)b * stride, n, s, seg, 1, sink, bwt_out + (size_t)b * stride,
-                         orig_out + b);
+        wave_sort_bucket2(blocks + (size_t)b * stride, n, s, seg, sink, bwt_out + (size_t)b * stride, orig_out + b,
+                          lds[wave_id()]);
     }
 }
 

@@ -61,12 +61,15 @@ struct LaneRun {
 };
 
 // Lane-serial move-to-front over [c0, c1) with the list held in W registers
-// (W*4 >= alphabet).  One fused pass per symbol: every word before the match
-// is shifted up one byte (v_alignbyte with the previous word), the matching
-// word is merged up to the match, later words are kept.  When a word has no
-// match, mask = all ones and the merge is the full shift, so the found / not
-// found cases need no branch; a wave-uniform early exit every 8 words stops
-// once every lane has found its symbol.
+// (W*4 >= alphabet).  Per symbol, two passes over the list words:
+//   search: SWAR zero-byte test of word ^ v*0x01010101; the first word with a
+//     match gives the position (fw, byte); stops once every lane has found
+//     its symbol;
+//   shift: words before fw move up one byte (v_alignbyte with the previous
+//     word), word fw is merged up to the match (v_perm with a per-symbol
+//     selector), later words stay; stops after the largest fw of the wave.
+// The wave-uniform bounds make text (small ranks) cheap; random data costs
+// about 11 VALU per list word.
 template <int W>
 __device__ void mtf_pass(const uint32_t* Lw, const uint8_t* __restrict__ X, uint8_t* __restrict__ R, int c0, int c1,
                          uint32_t* hist, LaneRun& st) {
@@ -74,58 +77,93 @@ __device__ void mtf_pass(const uint32_t* Lw, const uint8_t* __restrict__ X, uint
 #pragma unroll
     for (int j = 0; j < W; ++j) L[j] = Lw[j];
     uint32_t run = 0;
-    uint32_t pack = 0;
-    uint32_t xw = 0;
-    for (int i = c0; i < c1; ++i) {
-        if ((i & 3) == 0 || i == c0) xw = *(const uint32_t*)(X + (i & ~3));
-        const uint32_t v = (xw >> ((i & 3) * 8)) & 0xffu;
-        const uint32_t vv = v * 0x01010101u;
-        uint32_t prev = v << 24;
-        bool done = false;
-        uint32_t nbefore = 0, zf = 0;
-        bool all_done = false;
+    const int ntile = (int)uniform((uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max((uint32_t)((c1 - c0 + 15) >> 4)), 63));
+    // tiles of 16 symbols: one 16-byte load of X, one 16-byte store of ranks
+    for (int tile = 0; tile < ntile; ++tile) {
+        const int base = c0 + tile * 16;
+        uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
+        if (base < c1) {
+            const uint4 xin = *reinterpret_cast<const uint4*>(X + base);
+            x0 = xin.x;
+            x1 = xin.y;
+            x2 = xin.z;
+            x3 = xin.w;
+        }
+        uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, rc = 0;
+        for (int q = 0; q < 16; ++q) {
+            const bool live = base + q < c1;
+            const uint32_t v = x0 & 0xffu;
+            x0 >>= 8;
+            const uint32_t vv = v * 0x01010101u;
+            // ---- search: first word holding v
+            bool found = !live;
+            int fw = -1;
+            uint32_t zf = 0;
 #pragma unroll
-        for (int g = 0; g < W / 8; ++g) {
-            if (!all_done) {  // wave-uniform: skip the rest once every lane has found its symbol
+            for (int g = 0; g < W / 8; ++g) {
+                if (__ballot(!found)) {  // wave-uniform: stop once every lane has found its symbol
 #pragma unroll
-                for (int jj = 0; jj < 8; ++jj) {
-                    const int j = g * 8 + jj;
-                    const uint32_t w = L[j];
-                    const uint32_t x = w ^ vv;
-                    const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
-                    const uint32_t sh = __builtin_amdgcn_alignbyte(w, prev, 3);
-                    const uint32_t lowest = z & (0u - z);
-                    const uint32_t mask = (lowest << 1) - 1u;
-                    const uint32_t merged = (sh & mask) | (w & ~mask);
-                    L[j] = done ? w : merged;
-                    zf = done ? zf : z;
-                    nbefore += done ? 0u : 1u;
-                    done = done || (z != 0u);
-                    prev = w;
+                    for (int jj = 0; jj < 8; ++jj) {
+                        const int j = g * 8 + jj;
+                        const uint32_t xx = L[j] ^ vv;
+                        const uint32_t z = (xx - 0x01010101u) & ~xx & 0x80808080u;
+                        const bool hit = (z != 0u) && !found;
+                        fw = hit ? j : fw;
+                        zf = hit ? z : zf;
+                        found = found || (z != 0u);
+                    }
                 }
-                all_done = __all(done);
+            }
+            const uint32_t qb = (uint32_t)__builtin_ctz(zf | 0x80000000u) >> 3;  // byte of the match
+            // ---- shift: v_perm byte selects (0-3 = previous word, 4-7 = this word):
+            // words before fw move up one byte, word fw up to byte qb, later words stay
+            constexpr uint32_t keep = 0x07060504u, full = 0x06050403u;
+            const uint32_t qmask = qb >= 3 ? 0xffffffffu : ((1u << (8 * (qb + 1))) - 1u);
+            const uint32_t selq = (full & qmask) | (keep & ~qmask);
+            const int top = (int)__builtin_amdgcn_readlane((int)wave_incl_max((uint32_t)(fw + 1)), 63) - 1;
+            uint32_t prev = v << 24;
+#pragma unroll
+            for (int g = 0; g < W / 8; ++g) {
+                if (g * 8 <= top) {  // wave-uniform bound: the largest fw
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) {
+                        const int j = g * 8 + jj;
+                        const uint32_t w = L[j];
+                        const uint32_t sel = j < fw ? full : (j == fw ? selq : keep);
+                        L[j] = __builtin_amdgcn_perm(w, prev, sel);
+                        prev = w;
+                    }
+                }
+            }
+            const uint32_t pos = live ? 4u * (uint32_t)fw + qb : 0u;
+            rc |= pos << ((q & 3) * 8);
+            if ((q & 3) == 3) {  // (uniform) next source / result dword
+                x0 = x1;
+                x1 = x2;
+                x2 = x3;
+                r0 = r1;
+                r1 = r2;
+                r2 = r3;
+                r3 = rc;
+                rc = 0;
+            }
+            if (live) {
+                if (pos == 0) {
+                    run++;
+                } else {
+                    if (run > 0) {
+                        if (st.seen_nz) run_digits(run, st.ia, st.ib, st.idig);
+                        else st.zl = run;
+                        run = 0;
+                    }
+                    st.seen_nz = true;
+                    st.nz++;
+                    atomicAdd(&hist[pos + 1], 1u);
+                }
             }
         }
-        const uint32_t pos = 4u * (nbefore - 1u) + ((uint32_t)__builtin_ctz(zf) >> 3);
-        pack |= pos << ((i & 3) * 8);
-        if ((i & 3) == 3) {
-            *(uint32_t*)(R + (i & ~3)) = pack;
-            pack = 0;
-        }
-        if (pos == 0) {
-            run++;
-        } else {
-            if (run > 0) {
-                if (st.seen_nz) run_digits(run, st.ia, st.ib, st.idig);
-                else st.zl = run;
-                run = 0;
-            }
-            st.seen_nz = true;
-            st.nz++;
-            atomicAdd(&hist[pos + 1], 1u);
-        }
+        if (base < c1) *reinterpret_cast<uint4*>(R + base) = make_uint4(r0, r1, r2, r3);
     }
-    if (c1 > c0 && (c1 & 3)) *(uint32_t*)(R + (c1 & ~3)) = pack;
     if (run > 0) {
         st.zt = run;
         if (!st.seen_nz) st.zl = run;
@@ -159,14 +197,14 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     const int n = (int)lens[b];
     const uint8_t* X = bwt + (size_t)b * stride;
     uint8_t* R = ranks + (size_t)b * stride;
-    // per block: 64 recency lists, then 64 initial MTF lists (256 bytes each)
-    uint8_t* myrec = rec + ((size_t)b * NL * 2 + c) * 256;
+    // per block: 64 initial MTF lists (256 bytes each) in global scratch
+    // (the recency lists live in LDS)
     uint16_t* out = mtf_out + (size_t)b * mtf_stride;
     const bool stamp = b == nblocks / 2;
     BZ2MI_PHASE(g_mtf_phase, 0, stamp);
 
     int L = (n + NL - 1) / NL;
-    L = (L + 3) & ~3;
+    L = (L + 15) & ~15;  // 16-byte tiles
     const int c0 = min(c * L, n);
     const int c1 = min(c0 + L, n);
 
@@ -174,15 +212,34 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     for (int q = 0; q < 8; ++q) sh.mask[c][q] = 0;
     for (int s = c; s < kMaxAlpha; s += NL) sh.hist[s] = 0;
     int rcnt = 0;
-    for (int i = c1 - 1; i >= c0; --i) {
-        const uint32_t v = X[i];
-        const uint32_t bit = 1u << (v & 31);
-        uint32_t m = sh.mask[c][v >> 5];
-        if (!(m & bit)) {
-            sh.mask[c][v >> 5] = m | bit;
-            myrec[rcnt++] = (uint8_t)v;
+    uint4* myrec = reinterpret_cast<uint4*>(rec + ((size_t)b * NL * 2 + c) * 256);
+    uint32_t rb0 = 0, rb1 = 0, rb2 = 0, rb3 = 0;  // 16 pending list bytes
+    for (int base = c0 + (((c1 - c0 + 15) >> 4) - 1) * 16; base >= c0; base -= 16) {
+        const uint4 xin = *reinterpret_cast<const uint4*>(X + base);
+        const uint32_t xw[4] = {xin.x, xin.y, xin.z, xin.w};
+#pragma unroll
+        for (int q = 15; q >= 0; --q) {
+            if (base + q >= c1) continue;
+            const uint32_t v = (xw[q >> 2] >> ((q & 3) * 8)) & 0xffu;
+            const uint32_t bit = 1u << (v & 31);
+            const uint32_t m = sh.mask[c][v >> 5];
+            if (!(m & bit)) {
+                sh.mask[c][v >> 5] = m | bit;
+                const int sl = rcnt & 15;
+                const uint32_t add = v << ((sl & 3) * 8);
+                rb0 |= sl < 4 ? add : 0u;
+                rb1 |= (sl >> 2) == 1 ? add : 0u;
+                rb2 |= (sl >> 2) == 2 ? add : 0u;
+                rb3 |= (sl >> 2) == 3 ? add : 0u;
+                if (sl == 15) {
+                    myrec[rcnt >> 4] = make_uint4(rb0, rb1, rb2, rb3);
+                    rb0 = rb1 = rb2 = rb3 = 0;
+                }
+                rcnt++;
+            }
         }
     }
+    if (rcnt & 15) myrec[rcnt >> 4] = make_uint4(rb0, rb1, rb2, rb3);
     __syncthreads();
     if (c < 8) {
         uint32_t p = 0;
@@ -210,11 +267,25 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
         len++;
     };
     for (int cc = c - 1; cc >= 0 && len < k; --cc) {
-        const uint8_t* r = rec + ((size_t)b * NL * 2 + cc) * 256;
+        const uint4* r4 = reinterpret_cast<const uint4*>(rec + ((size_t)b * NL * 2 + cc) * 256);
         int cnt = 0;
         for (int q = 0; q < 8; ++q) cnt += __popc(sh.mask[cc][q]);
+        uint32_t rw[4] = {0, 0, 0, 0};
         for (int j = 0; j < cnt; ++j) {
-            const uint32_t v = r[j];
+            if ((j & 15) == 0) {
+                const uint4 t4 = r4[j >> 4];
+                rw[0] = t4.x;
+                rw[1] = t4.y;
+                rw[2] = t4.z;
+                rw[3] = t4.w;
+            }
+            const uint32_t v = rw[0] & 0xffu;  // consumed front to back
+            rw[0] >>= 8;
+            if ((j & 3) == 3) {
+                rw[0] = rw[1];
+                rw[1] = rw[2];
+                rw[2] = rw[3];
+            }
             const uint32_t bit = 1u << (v & 31);
             bool had = false;
 #pragma unroll
@@ -297,17 +368,24 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
         int i = c0;
         if (!own_lead && (zl > 0 || !seen_nz)) i = c0 + (int)zl;  // tail of an earlier lane's run
         bool lead = own_lead;
-        for (; i < c1; ++i) {
-            const uint32_t r = R[i];
-            if (r == 0) {
-                run++;
-            } else {
-                if (run > 0) {
-                    emit_run(lead ? lead_len : run, out, o);
-                    run = 0;
+        const int i0 = i;
+        for (int base = i0 & ~15; base < c1; base += 16) {  // 16-byte tiles of ranks
+            const uint4 rin = *reinterpret_cast<const uint4*>(R + base);
+            const uint32_t rw[4] = {rin.x, rin.y, rin.z, rin.w};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                if (base + q < i0 || base + q >= c1) continue;
+                const uint32_t r = (rw[q >> 2] >> ((q & 3) * 8)) & 0xffu;
+                if (r == 0) {
+                    run++;
+                } else {
+                    if (run > 0) {
+                        emit_run(lead ? lead_len : run, out, o);
+                        run = 0;
+                    }
+                    lead = false;
+                    out[o++] = (uint16_t)(r + 1);
                 }
-                lead = false;
-                out[o++] = (uint16_t)(r + 1);
             }
         }
         if (run > 0) emit_run(lead ? lead_len : tail_len, out, o);
