@@ -95,22 +95,35 @@ __device__ void mtf_pass(const uint32_t* Lw, const uint8_t* __restrict__ X, uint
             const uint32_t v = x0 & 0xffu;
             x0 >>= 8;
             const uint32_t vv = v * 0x01010101u;
-            // ---- search: first word holding v
-            bool found = !live;
+            // ---- search: first word holding v.  Wide lists (random-like data)
+            // scan every word, last to first, so the first hit simply wins;
+            // narrower ones scan forward and stop once every lane has found.
             int fw = -1;
             uint32_t zf = 0;
+            if constexpr (W == 64) {
 #pragma unroll
-            for (int g = 0; g < W / 8; ++g) {
-                if (__ballot(!found)) {  // wave-uniform: stop once every lane has found its symbol
+                for (int j = W - 1; j >= 0; --j) {
+                    const uint32_t xx = L[j] ^ vv;
+                    const uint32_t z = (xx - 0x01010101u) & ~xx & 0x80808080u;
+                    fw = z ? j : fw;
+                    zf = z ? z : zf;
+                }
+                if (!live) fw = -1;
+            } else {
+                bool found = !live;
 #pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) {
-                        const int j = g * 8 + jj;
-                        const uint32_t xx = L[j] ^ vv;
-                        const uint32_t z = (xx - 0x01010101u) & ~xx & 0x80808080u;
-                        const bool hit = (z != 0u) && !found;
-                        fw = hit ? j : fw;
-                        zf = hit ? z : zf;
-                        found = found || (z != 0u);
+                for (int g = 0; g < W / 8; ++g) {
+                    if (__ballot(!found)) {  // wave-uniform early exit
+#pragma unroll
+                        for (int jj = 0; jj < 8; ++jj) {
+                            const int j = g * 8 + jj;
+                            const uint32_t xx = L[j] ^ vv;
+                            const uint32_t z = (xx - 0x01010101u) & ~xx & 0x80808080u;
+                            const bool hit = (z != 0u) && !found;
+                            fw = hit ? j : fw;
+                            zf = hit ? z : zf;
+                            found = found || (z != 0u);
+                        }
                     }
                 }
             }
@@ -122,6 +135,7 @@ __device__ void mtf_pass(const uint32_t* Lw, const uint8_t* __restrict__ X, uint
             const uint32_t selq = (full & qmask) | (keep & ~qmask);
             const int top = (int)__builtin_amdgcn_readlane((int)wave_incl_max((uint32_t)(fw + 1)), 63) - 1;
             uint32_t prev = v << 24;
+            uint32_t state = fw >= 0 ? full : keep;
 #pragma unroll
             for (int g = 0; g < W / 8; ++g) {
                 if (g * 8 <= top) {  // wave-uniform bound: the largest fw
@@ -129,7 +143,9 @@ __device__ void mtf_pass(const uint32_t* Lw, const uint8_t* __restrict__ X, uint
                     for (int jj = 0; jj < 8; ++jj) {
                         const int j = g * 8 + jj;
                         const uint32_t w = L[j];
-                        const uint32_t sel = j < fw ? full : (j == fw ? selq : keep);
+                        const bool at = j == fw;
+                        const uint32_t sel = at ? selq : state;  // full before fw, keep after
+                        state = at ? keep : state;
                         L[j] = __builtin_amdgcn_perm(w, prev, sel);
                         prev = w;
                     }
