@@ -48,40 +48,16 @@ int dalloc(T** p, size_t count) {
 
 }  // namespace
 
-struct bz2mi_ctx {
-    int level = 9, p = 10, unit = 10000, S = 90000, device = 0;
-    size_t stride = 0;           // device bytes per block slot
-    size_t mtf_stride = 0;       // uint16 per block
-    size_t payload_words = 0;    // uint32 per block
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
-    int cap = 0;                 // blocks the batch buffers hold
-    int bwt_slots = 0;
-    int batch_blocks = 16384;  // blocks per back-end batch
-    bool want_stats = false;
-
+// Device buffers of one batch of blocks (RLE1 input to Huffman payloads).
+// The pipelined compress_device keeps kSets of them in flight.
+struct Batch {
+    int cap = 0;  // blocks
     uint8_t* d_blocks = nullptr;
     uint32_t* d_lens = nullptr;
     uint32_t* d_crc = nullptr;
     uint8_t* d_bwt = nullptr;
     uint32_t* d_orig = nullptr;
-    uint8_t* d_ranks = nullptr;
-    uint8_t* d_rec = nullptr;
-    uint16_t* d_mtf = nullptr;
-    uint32_t* d_mtflen = nullptr;
-    uint32_t* d_alpha = nullptr;
-    uint32_t* d_hist = nullptr;
-    uint32_t* d_present = nullptr;
-    uint32_t* d_seed = nullptr;
-    uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
-    uint32_t* d_payload = nullptr;
-    uint64_t* d_pbits = nullptr;
-    uint64_t* d_offs = nullptr;
-    uint32_t* d_out = nullptr;
-    size_t out_words = 0;
-    uint8_t* d_scratch = nullptr;
-    uint32_t* d_counter = nullptr;
-    // BWT split (bwt.hip): per-block SA, bucket queue, per-block group lists
+    // BWT (bwt.hip): per-block SA, bucket queue, large-bucket lists, group lists
     uint32_t* d_sa = nullptr;
     uint64_t* d_bq = nullptr;
     uint32_t* d_bcnt = nullptr;  // [0] queued buckets, [1] blocks with large buckets, [2] blocks with
@@ -92,8 +68,54 @@ struct bz2mi_ctx {
     uint32_t* d_clist = nullptr;
     uint32_t* d_p2list = nullptr;
     bz2mi::BwtSeg* d_groups = nullptr;
+    // MTF / Huffman
+    uint8_t* d_ranks = nullptr;
+    uint8_t* d_rec = nullptr;
+    uint16_t* d_mtf = nullptr;
+    uint32_t* d_mtflen = nullptr;
+    uint32_t* d_alpha = nullptr;
+    uint32_t* d_hist = nullptr;
+    uint32_t* d_present = nullptr;
+    uint32_t* d_seed = nullptr;
+    uint32_t* d_payload = nullptr;
+    uint64_t* d_pbits = nullptr;
+    uint64_t* d_offs = nullptr;
+    // pipeline hand-offs: stage A done, MTF done, buffers free again
+    hipEvent_t evA = nullptr, evM = nullptr, evFree = nullptr;
+
+    std::vector<void*> ptrs() const {
+        return {d_blocks, d_lens, d_crc, d_bwt, d_orig, d_sa, d_bq, d_bcnt, d_large, d_nlarge, d_ngroups, d_clist,
+                d_p2list, d_groups, d_ranks, d_rec, d_mtf, d_mtflen, d_alpha, d_hist, d_present, d_seed, d_payload,
+                d_pbits, d_offs};
+    }
+};
+
+constexpr int kSets = 3;
+
+struct bz2mi_ctx {
+    int level = 9, p = 10, unit = 10000, S = 90000, device = 0;
+    size_t stride = 0;           // device bytes per block slot
+    size_t mtf_stride = 0;       // uint16 per block
+    size_t payload_words = 0;    // uint32 per block
+    hipStream_t stream = nullptr;  // front end and the host-driven entry points
+    hipStream_t sA = nullptr, sM = nullptr, sB = nullptr;  // pipeline: RLE1+CRC+BWT / MTF / Huffman+assembly
+    bool own_stream = false;
     int cus = 256;
+    int bwt_slots = 0;
+    int batch_blocks = 0;  // blocks per pipelined batch (0: from the block size)
+    bool want_stats = false;
+
+    Batch sets[kSets];
+    uint32_t* d_out = nullptr;   // staging for the host-driven assembly
+    size_t out_words = 0;
+    uint8_t* d_scratch = nullptr;  // BWT workgroup slots (one BWT runs at a time: stream sA)
+    uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
     uint32_t* d_crctab = nullptr;
+    bz2mi::StreamDev* d_sd = nullptr;
+    unsigned long long* d_vol = nullptr;  // [3] volumes of the last compress_device call
+    bz2mi::StreamDev h_sd{};
+    uint8_t* d_ostage = nullptr;   // aligned output staging for unaligned destinations
+    size_t ostage_cap = 0;
     // front-end buffers (device RLE1 path)
     size_t fe_n = 0;
     uint8_t* d_in = nullptr;        // staging for host input
@@ -109,10 +131,11 @@ struct bz2mi_ctx {
     uint64_t* d_nb = nullptr;
     size_t fe_maxb = 0;
     hipEvent_t ev[8] = {};
+    std::vector<hipEvent_t> tev;  // per-batch stage timing events (12 per batch)
     float last_ms[6] = {0, 0, 0, 0, 0, 0};
     uint64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
-    // stream state (OutputStream.hpp:39-44)
+    // stream state of the host-driven path (OutputStream.hpp:39-44)
     uint64_t blocks_done = 0;
     uint32_t stream_crc = 0;
     uint64_t carry = 0;      // MSB-aligned pending bits
@@ -143,87 +166,140 @@ bool sync_debug() {
         }                                                                             \
     } while (0)
 
-int ensure_capacity(bz2mi_ctx* c, int nblocks) {
-    if (nblocks <= c->cap) return BZ2MI_OK;
-    int cap = std::max(nblocks, 16);
+int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks) {
+    if (nblocks <= t.cap) return BZ2MI_OK;
+    const int cap = std::max(nblocks, 16);
     const size_t B = (size_t)cap;
     int r;
-    if ((r = dalloc(&c->d_blocks, B * c->stride))) return r;
-    if ((r = dalloc(&c->d_lens, B))) return r;
-    if ((r = dalloc(&c->d_crc, B))) return r;
-    if ((r = dalloc(&c->d_bwt, B * c->stride))) return r;
-    if ((r = dalloc(&c->d_orig, B))) return r;
-    if ((r = dalloc(&c->d_sa, B * c->stride))) return r;
-    if ((r = dalloc(&c->d_bq, B * 256))) return r;
-    if ((r = dalloc(&c->d_large, B * 256))) return r;
-    if ((r = dalloc(&c->d_nlarge, B))) return r;
-    if ((r = dalloc(&c->d_ngroups, B))) return r;
-    if ((r = dalloc(&c->d_clist, B))) return r;
-    if ((r = dalloc(&c->d_p2list, B))) return r;
-    if ((r = dalloc(&c->d_groups, B * bz2mi::bwt_group_stride(c->stride)))) return r;
-    if ((r = dalloc(&c->d_ranks, B * c->stride))) return r;
-    if ((r = dalloc(&c->d_rec, B * 64 * 512))) return r;
-    if ((r = dalloc(&c->d_mtf, B * c->mtf_stride))) return r;
-    if ((r = dalloc(&c->d_mtflen, B))) return r;
-    if ((r = dalloc(&c->d_alpha, B))) return r;
-    if ((r = dalloc(&c->d_hist, B * bz2mi::kMaxAlpha))) return r;
-    if ((r = dalloc(&c->d_present, B * 8))) return r;
-    if ((r = dalloc(&c->d_seed, B * bz2mi::kMaxAlpha))) return r;
-    if ((r = dalloc(&c->d_payload, B * c->payload_words))) return r;
-    if ((r = dalloc(&c->d_pbits, B))) return r;
-    if ((r = dalloc(&c->d_offs, B + 1))) return r;
-    c->out_words = B * (c->payload_words + 4) + 64;
-    if ((r = dalloc(&c->d_out, c->out_words))) return r;
-    c->cap = cap;
+    if ((r = dalloc(&t.d_blocks, B * c->stride))) return r;
+    if ((r = dalloc(&t.d_lens, B))) return r;
+    if ((r = dalloc(&t.d_crc, B))) return r;
+    if ((r = dalloc(&t.d_bwt, B * c->stride))) return r;
+    if ((r = dalloc(&t.d_orig, B))) return r;
+    if ((r = dalloc(&t.d_sa, B * c->stride))) return r;
+    if ((r = dalloc(&t.d_bq, B * 256))) return r;
+    if ((r = dalloc(&t.d_bcnt, 8))) return r;
+    if ((r = dalloc(&t.d_large, B * 256))) return r;
+    if ((r = dalloc(&t.d_nlarge, B))) return r;
+    if ((r = dalloc(&t.d_ngroups, B))) return r;
+    if ((r = dalloc(&t.d_clist, B))) return r;
+    if ((r = dalloc(&t.d_p2list, B))) return r;
+    if ((r = dalloc(&t.d_groups, B * bz2mi::bwt_group_stride(c->stride)))) return r;
+    if ((r = dalloc(&t.d_ranks, B * c->stride))) return r;
+    if ((r = dalloc(&t.d_rec, B * 64 * 512))) return r;
+    if ((r = dalloc(&t.d_mtf, B * c->mtf_stride))) return r;
+    if ((r = dalloc(&t.d_mtflen, B))) return r;
+    if ((r = dalloc(&t.d_alpha, B))) return r;
+    if ((r = dalloc(&t.d_hist, B * bz2mi::kMaxAlpha))) return r;
+    if ((r = dalloc(&t.d_present, B * 8))) return r;
+    if ((r = dalloc(&t.d_seed, B * bz2mi::kMaxAlpha))) return r;
+    if ((r = dalloc(&t.d_payload, B * c->payload_words))) return r;
+    if ((r = dalloc(&t.d_pbits, B))) return r;
+    if ((r = dalloc(&t.d_offs, B + 1))) return r;
+    if (!t.evA) {
+        HIPCHECK(hipEventCreateWithFlags(&t.evA, hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&t.evM, hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&t.evFree, hipEventDisableTiming));
+    }
+    t.cap = cap;
     return BZ2MI_OK;
 }
 
-// Kernel sequence for `nb` RLE1 blocks already in d_blocks/d_lens/d_crc.
-// Produces d_payload/d_pbits (and, with assemble, d_out).
-int run_blocks(bz2mi_ctx* c, int nb) {
+// host-driven paths: batch set 0 plus the assembly staging buffer
+int ensure_capacity(bz2mi_ctx* c, int nblocks) {
+    int r;
+    if ((r = ensure_batch(c, c->sets[0], nblocks))) return r;
+    const size_t words = (size_t)c->sets[0].cap * (c->payload_words + 4) + 64;
+    if (words > c->out_words) {
+        if ((r = dalloc(&c->d_out, words))) return r;
+        c->out_words = words;
+    }
+    return BZ2MI_OK;
+}
+
+// ---- the stages of one batch, each on its stream
+// RLE1 emission + block CRCs of blocks [first, first+cnt) of the front end
+int stage_front(bz2mi_ctx* c, Batch& t, const uint8_t* d_x, size_t n, uint64_t first, uint64_t cnt, hipStream_t s) {
     using namespace bz2mi;
-    hipStream_t s = c->stream;
-    (void)hipGetLastError();
-    HIPCHECK(hipEventRecord(c->ev[0], s));
-    HIPCHECK(hipMemsetAsync(c->d_bcnt, 0, 8 * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(fe_rle1_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts, first,
+                       cnt, t.d_blocks, c->stride, t.d_lens);
+    hipLaunchKernelGGL(fe_crc_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts, first, cnt,
+                       t.d_crc, c->d_crctab);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("front-rle1");
+    return BZ2MI_OK;
+}
+
+int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
+    using namespace bz2mi;
+    HIPCHECK(hipMemsetAsync(t.d_bcnt, 0, 8 * sizeof(uint32_t), s));
     const int slots = std::min(nb, c->bwt_slots);
-    hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens, nb, c->d_sa,
-                       c->d_bwt, c->d_orig, c->d_bq, c->d_bcnt, c->d_large, c->d_nlarge, c->d_ngroups, c->d_clist,
-                       c->d_bcnt + 1);
+    hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
+                       t.d_bwt, t.d_orig, t.d_bq, t.d_bcnt, t.d_large, t.d_nlarge, t.d_ngroups, t.d_clist,
+                       t.d_bcnt + 1);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");
-    hipLaunchKernelGGL(bwt_small_kernel, dim3(c->cus * 8), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens,
-                       c->d_sa, c->d_bwt, c->d_orig, c->d_bq, c->d_bcnt, c->d_groups, c->d_ngroups, c->d_p2list,
-                       c->d_bcnt + 2);
+    hipLaunchKernelGGL(bwt_small_kernel, dim3(c->cus * 8), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, t.d_sa,
+                       t.d_bwt, t.d_orig, t.d_bq, t.d_bcnt, t.d_groups, t.d_ngroups, t.d_p2list, t.d_bcnt + 2);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_small");
-    hipLaunchKernelGGL(bwt_large_kernel, dim3(slots), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens, nb,
-                       c->d_sa, c->d_bwt, c->d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, c->d_large,
-                       c->d_nlarge, c->d_groups, c->d_ngroups, c->d_p2list, c->d_bcnt + 2, c->d_clist,
-                       c->d_bcnt + 1, c->d_bcnt + 3);
+    hipLaunchKernelGGL(bwt_large_kernel, dim3(slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
+                       t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, t.d_large, t.d_nlarge,
+                       t.d_groups, t.d_ngroups, t.d_p2list, t.d_bcnt + 2, t.d_clist, t.d_bcnt + 1, t.d_bcnt + 3);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_large");
-    hipLaunchKernelGGL(bwt_double_kernel, dim3(slots), dim3(256), 0, s, c->d_blocks, c->stride, c->d_lens, nb,
-                       c->d_sa, c->d_bwt, c->d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, c->d_groups,
-                       c->d_ngroups, c->d_p2list, c->d_bcnt + 2, c->d_bcnt + 4);
+    hipLaunchKernelGGL(bwt_double_kernel, dim3(slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
+                       t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, t.d_groups, t.d_ngroups,
+                       t.d_p2list, t.d_bcnt + 2, t.d_bcnt + 4);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt");
-    HIPCHECK(hipEventRecord(c->ev[1], s));
-    hipLaunchKernelGGL(mtf_kernel, dim3(nb), dim3(64), 0, s, c->d_bwt, c->stride, c->d_lens, nb, c->d_ranks,
-                       c->d_rec, c->d_mtf, c->mtf_stride, c->d_mtflen, c->d_alpha, c->d_hist, c->d_present);
+    return BZ2MI_OK;
+}
+
+int stage_mtf(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
+    using namespace bz2mi;
+    hipLaunchKernelGGL(mtf_kernel, dim3(nb), dim3(64), 0, s, t.d_bwt, c->stride, t.d_lens, nb, t.d_ranks, t.d_rec,
+                       t.d_mtf, c->mtf_stride, t.d_mtflen, t.d_alpha, t.d_hist, t.d_present);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("mtf");
-    HIPCHECK(hipEventRecord(c->ev[2], s));
+    return BZ2MI_OK;
+}
+
+int stage_seed(bz2mi_ctx* c, Batch& t, int nb, uint64_t first_block, hipStream_t s) {
+    using namespace bz2mi;
     const int ne = c->p * kMaxAlpha;
-    hipLaunchKernelGGL(seed_kernel, dim3((ne + 255) / 256), dim3(256), 0, s, c->d_hist, c->d_seed, c->d_state, nb,
-                       c->p, (uint64_t)c->blocks_done);
+    hipLaunchKernelGGL(seed_kernel, dim3((ne + 255) / 256), dim3(256), 0, s, t.d_hist, t.d_seed, c->d_state, nb, c->p,
+                       first_block);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("seed");
-    HIPCHECK(hipEventRecord(c->ev[3], s));
-    hipLaunchKernelGGL(huffman_kernel, dim3(nb), dim3(256), 0, s, c->d_mtf, c->mtf_stride, c->d_mtflen, c->d_alpha,
-                       c->d_seed, c->d_present, c->d_orig, nb, c->d_payload, c->payload_words, c->d_pbits);
+    return BZ2MI_OK;
+}
+
+int stage_huffman(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
+    using namespace bz2mi;
+    hipLaunchKernelGGL(huffman_kernel, dim3(nb), dim3(256), 0, s, t.d_mtf, c->mtf_stride, t.d_mtflen, t.d_alpha,
+                       t.d_seed, t.d_present, t.d_orig, nb, t.d_payload, c->payload_words, t.d_pbits);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("huffman");
+    return BZ2MI_OK;
+}
+
+// Host-driven kernel sequence for `nb` RLE1 blocks already in set 0
+// (d_blocks/d_lens/d_crc), all on the context stream.  Produces
+// d_payload/d_pbits.
+int run_blocks(bz2mi_ctx* c, int nb) {
+    hipStream_t s = c->stream;
+    Batch& t = c->sets[0];
+    int r;
+    (void)hipGetLastError();
+    HIPCHECK(hipEventRecord(c->ev[0], s));
+    if ((r = stage_bwt(c, t, nb, s))) return r;
+    HIPCHECK(hipEventRecord(c->ev[1], s));
+    if ((r = stage_mtf(c, t, nb, s))) return r;
+    HIPCHECK(hipEventRecord(c->ev[2], s));
+    if ((r = stage_seed(c, t, nb, c->blocks_done, s))) return r;
+    HIPCHECK(hipEventRecord(c->ev[3], s));
+    if ((r = stage_huffman(c, t, nb, s))) return r;
     HIPCHECK(hipEventRecord(c->ev[4], s));
     return BZ2MI_OK;
 }
@@ -243,16 +319,16 @@ int assemble_to(bz2mi_ctx* c, int nb, bool final_, uint32_t* dst, size_t dst_byt
         prefix_bits = 32;
     }
     (void)hipGetLastError();
-    hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(256), 0, s, c->d_pbits, nb, (uint64_t)prefix_bits, c->d_offs);
+    hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(256), 0, s, c->sets[0].d_pbits, nb, (uint64_t)prefix_bits, c->sets[0].d_offs);
     HIPCHECK(hipGetLastError());
     uint64_t end_bits = 0;
-    HIPCHECK(hipMemcpyAsync(&end_bits, c->d_offs + nb, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipMemcpyAsync(&end_bits, c->sets[0].d_offs + nb, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
     if (final_) end_bits += 80;
     const uint64_t words = (end_bits + 31) / 32;
     if (words * 4 > dst_bytes) return fail(BZ2MI_ESPACE, "output buffer too small");
-    hipLaunchKernelGGL(assemble_kernel, dim3(nb + 2), dim3(256), 0, s, c->d_payload, c->payload_words, c->d_offs,
-                       c->d_crc, nb, prefix, prefix_bits, final_ ? 1 : 0, c->stream_crc, dst);
+    hipLaunchKernelGGL(assemble_kernel, dim3(nb + 2), dim3(256), 0, s, c->sets[0].d_payload, c->payload_words, c->sets[0].d_offs,
+                       c->sets[0].d_crc, nb, prefix, prefix_bits, final_ ? 1 : 0, c->stream_crc, dst);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("assemble");
     HIPCHECK(hipEventRecord(c->ev[5], s));
@@ -319,8 +395,26 @@ void reset_stream(bz2mi_ctx* c) {
     (void)hipMemsetAsync(c->d_state, 0, sizeof(uint32_t) * c->p * bz2mi::kMaxAlpha, c->stream);
 }
 
-// Whole stream from device bytes: front end, back end in block batches,
-// assembly into d_out.  *out_len = stream bytes.
+// Per-batch stage timing: events 2*i / 2*i+1 bracket stage i of a batch
+// (0 RLE1+CRC, 1 BWT, 2 MTF, 3 seed, 4 Huffman, 5 assembly).
+hipEvent_t* batch_events(bz2mi_ctx* c, uint64_t k) {
+    const size_t need = (size_t)(k + 1) * 12;
+    while (c->tev.size() < need) {
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        c->tev.push_back(e);
+    }
+    return c->tev.data() + k * 12;
+}
+
+// Whole stream from device bytes.  Front end (RLE1 split) for the whole input
+// on the context stream, then the blocks in batches through a three-stream
+// pipeline: stream A runs RLE1 emission, block CRCs and the BWT of batch k
+// while stream M runs the MTF of batch k-1 and stream B the seeds, Huffman
+// coding and assembly of batch k-2 (the seed carry-over and the stream
+// offsets chain through stream B in batch order).  The stream state (bit
+// offset, carried partial word, stream CRC) stays on the device, so the host
+// waits once, for the final length.
 int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_out, size_t cap, size_t* out_len) {
     using namespace bz2mi;
     hipStream_t s = c->stream;
@@ -352,82 +446,111 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
         STAGE_DONE("front-resolve");
     }
     HIPCHECK(hipEventRecord(c->ev[7], s));
-    const uint64_t batch = (uint64_t)c->batch_blocks;
-    size_t o = 0;  // bytes of d_out written
-    std::vector<uint32_t> crcs;
-    for (uint64_t first = 0; first < nb || (nb == 0 && first == 0); first += batch) {
-        const uint64_t cnt = nb ? std::min(batch, nb - first) : 0;
-        const bool last = first + cnt >= nb;
-        if ((r = ensure_capacity(c, (int)std::max<uint64_t>(cnt, 1)))) return r;
-        if (cnt) {
-            hipLaunchKernelGGL(fe_rle1_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts,
-                               first, cnt, c->d_blocks, c->stride, c->d_lens);
-            hipLaunchKernelGGL(fe_crc_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts,
-                               first, cnt, c->d_crc, c->d_crctab);
-            HIPCHECK(hipGetLastError());
-            STAGE_DONE("front-rle1");
-            if ((r = run_blocks(c, (int)cnt))) return r;
-            crcs.resize(cnt);
-            HIPCHECK(hipMemcpyAsync(crcs.data(), c->d_crc, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-            HIPCHECK(hipStreamSynchronize(s));
-            for (uint64_t j = 0; j < cnt; ++j)
-                c->stream_crc = ((c->stream_crc << 1) | (c->stream_crc >> 31)) ^ crcs[j];
+    // batches
+    const uint64_t bsz = (uint64_t)c->batch_blocks;
+    const uint64_t nbat = nb ? (nb + bsz - 1) / bsz : 1;
+    const int sets_used = (int)std::min<uint64_t>(nbat, kSets);
+    for (int k = 0; k < sets_used; ++k)
+        if ((r = ensure_batch(c, c->sets[k], (int)std::max<uint64_t>(std::min(bsz, nb), 1)))) return r;
+    // output: word-aligned destination, else an aligned staging buffer
+    uint32_t* out32 = (uint32_t*)d_out;
+    const bool staged = ((uintptr_t)d_out & 3) != 0;
+    if (staged) {
+        if (cap + 8 > c->ostage_cap) {
+            if ((r = dalloc(&c->d_ostage, cap + 8))) return r;
+            c->ostage_cap = cap + 8;
         }
-        // assemble straight into d_out when it is word aligned there, else stage
-        uint64_t bits = 0;
-        const bool direct = o == 0 && c->carry_bits == 0 && ((uintptr_t)d_out & 3) == 0;
-        if (direct) {
-            if ((r = assemble_to(c, (int)cnt, last, (uint32_t*)d_out, cap & ~(size_t)3, &bits))) return r;
-        } else {
-            if ((r = assemble_to(c, (int)cnt, last, c->d_out, c->out_words * 4, &bits))) return r;
-        }
-        const size_t nbytes = (size_t)(bits >> 3);
-        const int rem = (int)(bits & 7);
-        if (o + nbytes + (rem ? 1 : 0) > cap) return fail(BZ2MI_ESPACE, "output buffer too small");
-        if (!direct)
-            HIPCHECK(hipMemcpyAsync(d_out + o, c->d_out, nbytes + (rem ? 1 : 0), hipMemcpyDeviceToDevice, s));
-        if (rem) {
-            uint8_t lastb = 0;
-            HIPCHECK(hipMemcpyAsync(&lastb, d_out + o + nbytes, 1, hipMemcpyDeviceToHost, s));
-            HIPCHECK(hipStreamSynchronize(s));
-            c->carry = ((uint64_t)lastb << 56) & (~0ull << (64 - rem));
-        } else {
-            c->carry = 0;
-        }
-        c->carry_bits = rem;
-        o += nbytes;
-        c->blocks_done += cnt;
-        record_timings(c, (int)cnt);
-        if (nb == 0) break;
+        out32 = (uint32_t*)c->d_ostage;
     }
-    HIPCHECK(hipStreamSynchronize(s));
+    const uint64_t cap_words = cap / 4;
+    // device stream state: the header "BZh<level>" (OutputStream.hpp:126-128) is carried in
+    c->h_sd = StreamDev{};
+    c->h_sd.carry = (0x425a68u << 8) | (uint32_t)('0' + c->level);
+    c->h_sd.carry_bits = 32;
+    HIPCHECK(hipMemcpyAsync(c->d_sd, &c->h_sd, sizeof(StreamDev), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipMemsetAsync(c->d_vol, 0, 4 * sizeof(unsigned long long), s));
+    HIPCHECK(hipEventRecord(c->ev[0], s));
+    HIPCHECK(hipStreamWaitEvent(c->sA, c->ev[0], 0));
+    HIPCHECK(hipStreamWaitEvent(c->sM, c->ev[0], 0));
+    HIPCHECK(hipStreamWaitEvent(c->sB, c->ev[0], 0));
+    for (uint64_t k = 0; k < nbat; ++k) {
+        Batch& t = c->sets[k % kSets];
+        const uint64_t first = k * bsz;
+        const uint64_t cnt = nb ? std::min(bsz, nb - first) : 0;
+        const bool last = k + 1 == nbat;
+        hipEvent_t* te = batch_events(c, k);
+        if (cnt) {
+            if (k >= (uint64_t)kSets) HIPCHECK(hipStreamWaitEvent(c->sA, t.evFree, 0));
+            HIPCHECK(hipEventRecord(te[0], c->sA));
+            if ((r = stage_front(c, t, d_x, n, first, cnt, c->sA))) return r;
+            HIPCHECK(hipEventRecord(te[1], c->sA));
+            HIPCHECK(hipEventRecord(te[2], c->sA));
+            if ((r = stage_bwt(c, t, (int)cnt, c->sA))) return r;
+            HIPCHECK(hipEventRecord(te[3], c->sA));
+            HIPCHECK(hipEventRecord(t.evA, c->sA));
+            HIPCHECK(hipStreamWaitEvent(c->sM, t.evA, 0));
+            HIPCHECK(hipEventRecord(te[4], c->sM));
+            if ((r = stage_mtf(c, t, (int)cnt, c->sM))) return r;
+            HIPCHECK(hipEventRecord(te[5], c->sM));
+            HIPCHECK(hipEventRecord(t.evM, c->sM));
+            HIPCHECK(hipStreamWaitEvent(c->sB, t.evM, 0));
+            HIPCHECK(hipEventRecord(te[6], c->sB));
+            if ((r = stage_seed(c, t, (int)cnt, first, c->sB))) return r;
+            HIPCHECK(hipEventRecord(te[7], c->sB));
+            HIPCHECK(hipEventRecord(te[8], c->sB));
+            if ((r = stage_huffman(c, t, (int)cnt, c->sB))) return r;
+            HIPCHECK(hipEventRecord(te[9], c->sB));
+            hipLaunchKernelGGL(volume_kernel, dim3(16), dim3(256), 0, c->sB, t.d_lens, t.d_mtflen, t.d_pbits, (int)cnt,
+                               c->d_vol);
+        }
+        HIPCHECK(hipEventRecord(te[10], c->sB));
+        hipLaunchKernelGGL(offsets_dev_kernel, dim3(1), dim3(256), 0, c->sB, t.d_pbits, t.d_crc, (int)cnt, c->d_sd,
+                           t.d_offs);
+        hipLaunchKernelGGL(assemble_dev_kernel, dim3((unsigned)cnt + 2), dim3(256), 0, c->sB, t.d_payload,
+                           c->payload_words, t.d_offs, t.d_crc, (int)cnt, last ? 1 : 0, c->d_sd, out32, cap_words);
+        hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, c->sB, t.d_offs, (int)cnt, last ? 1 : 0, c->d_sd,
+                           out32, cap_words);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipEventRecord(te[11], c->sB));
+        HIPCHECK(hipEventRecord(t.evFree, c->sB));
+    }
+    HIPCHECK(hipMemcpyAsync(&c->h_sd, c->d_sd, sizeof(StreamDev), hipMemcpyDeviceToHost, c->sB));
+    HIPCHECK(hipStreamSynchronize(c->sB));
+    const uint64_t bytes = (c->h_sd.final_bits + 7) / 8;
+    if (bytes > cap_words * 4) return fail(BZ2MI_ESPACE, "output buffer too small");
+    if (staged) HIPCHECK(hipMemcpy(d_out, c->d_ostage, bytes, hipMemcpyDeviceToDevice));
+    // stage times summed over the batches (stages of different batches overlap)
+    float fe_ms = 0;
+    if (hipEventElapsedTime(&fe_ms, c->ev[6], c->ev[7]) != hipSuccess) fe_ms = 0;
+    float sum[6] = {fe_ms, 0, 0, 0, 0, 0};
+    for (uint64_t k = 0; k < nbat; ++k) {
+        hipEvent_t* te = batch_events(c, k);
+        float ms;
+        if (nb) {
+            if (hipEventElapsedTime(&ms, te[0], te[1]) == hipSuccess) sum[0] += ms;
+            if (hipEventElapsedTime(&ms, te[2], te[3]) == hipSuccess) sum[1] += ms;
+            if (hipEventElapsedTime(&ms, te[4], te[5]) == hipSuccess) sum[2] += ms;
+            if (hipEventElapsedTime(&ms, te[6], te[7]) == hipSuccess) sum[3] += ms;
+            if (hipEventElapsedTime(&ms, te[8], te[9]) == hipSuccess) sum[4] += ms;
+        }
+        if (hipEventElapsedTime(&ms, te[10], te[11]) == hipSuccess) sum[5] += ms;
+    }
+    (void)hipGetLastError();
+    for (int i = 0; i < 6; ++i) c->last_ms[i] = sum[i];
     c->stats[0] = n;
     c->stats[1] = nb;
-    c->stats[5] = o;
-    if (c->want_stats && nb && nb <= (uint64_t)c->cap) {
-        // per-stage volumes of the last batch (single-batch runs: the whole stream)
-        const uint64_t cnt = nb - (nb - 1) / batch * batch;
-        std::vector<uint32_t> a(cnt), m(cnt);
-        std::vector<uint64_t> pb(cnt);
-        HIPCHECK(hipMemcpy(a.data(), c->d_lens, cnt * 4, hipMemcpyDeviceToHost));
-        HIPCHECK(hipMemcpy(m.data(), c->d_mtflen, cnt * 4, hipMemcpyDeviceToHost));
-        HIPCHECK(hipMemcpy(pb.data(), c->d_pbits, cnt * 8, hipMemcpyDeviceToHost));
-        uint64_t sa = 0, sm = 0, sp = 0;
-        for (uint64_t j = 0; j < cnt; ++j) {
-            sa += a[j];
-            sm += m[j];
-            sp += pb[j];
-        }
-        c->stats[2] = sa;
-        c->stats[3] = sm;
-        c->stats[4] = sp;
-        c->stats[6] = cnt;
+    c->stats[5] = bytes;
+    {
+        unsigned long long vol[4] = {0, 0, 0, 0};
+        HIPCHECK(hipMemcpy(vol, c->d_vol, sizeof(vol), hipMemcpyDeviceToHost));
+        c->stats[2] = vol[0];
+        c->stats[3] = vol[1];
+        c->stats[4] = vol[2];
+        c->stats[6] = nb;
     }
-    float fe_ms = 0;
-    if (hipEventElapsedTime(&fe_ms, c->ev[6], c->ev[7]) == hipSuccess) c->last_ms[0] = fe_ms;
-    (void)hipGetLastError();
+    c->blocks_done = nb;
     c->finished = true;
-    *out_len = o;
+    *out_len = bytes;
     return BZ2MI_OK;
 }
 
@@ -483,9 +606,12 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
         const size_t bits = 24 + 272 + 18 + (S / 50 + 1) * 6 + 6 * (5 + 258 * 39) + (S + 1) * 20;
         c->payload_words = (bits + 31) / 32 + 4;
     }
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->sA, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->sM, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->sB, hipStreamNonBlocking) != hipSuccess) {
         fail(BZ2MI_EDEVICE, "hipStreamCreate failed");
-        delete c;
+        bz2mi_destroy(c);
         return nullptr;
     }
     c->own_stream = true;
@@ -494,9 +620,8 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
     c->cus = cus;
     c->bwt_slots = cus * 4;
-    if (dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S)) || dalloc(&c->d_counter, 4) ||
-        dalloc(&c->d_bcnt, 8) ||
-        dalloc(&c->d_state, (size_t)c->p * bz2mi::kMaxAlpha)) {
+    if (dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S)) ||
+        dalloc(&c->d_state, (size_t)c->p * bz2mi::kMaxAlpha) || dalloc(&c->d_sd, 1) || dalloc(&c->d_vol, 4)) {
         bz2mi_destroy(c);
         return nullptr;
     }
@@ -506,6 +631,12 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
         bz2mi_destroy(c);
         return nullptr;
     }
+    // Batches of about 1.5 GB of block input (BZ2MI_BATCH_BLOCKS overrides).
+    // Measured on MI355X: the stage kernels are throughput-bound, so running
+    // them concurrently on smaller batches (the three-stream pipeline) was
+    // slower (1 GiB random: 17.1 GB/s in one batch, 16.2 in four, 15.3 in
+    // eight); the pipeline matters for inputs larger than one batch.
+    c->batch_blocks = std::min(16384, std::max(64, (int)((1536u << 20) / (unsigned)c->S)));
     if (const char* e = getenv("BZ2MI_BATCH_BLOCKS")) c->batch_blocks = std::max(1, atoi(e));
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     return c;
@@ -514,18 +645,25 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
 void bz2mi_destroy(bz2mi_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* ptrs[] = {c->d_blocks, c->d_lens, c->d_crc, c->d_bwt, c->d_orig, c->d_ranks, c->d_rec, c->d_mtf,
-                    c->d_mtflen, c->d_alpha, c->d_hist, c->d_present, c->d_seed, c->d_state, c->d_payload,
-                    c->d_pbits, c->d_offs, c->d_out, c->d_scratch, c->d_counter, c->d_crctab, c->d_in,
-                    c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd, c->d_starts, c->d_nb,
-                    c->d_sa, c->d_bq, c->d_bcnt, c->d_large, c->d_nlarge, c->d_ngroups, c->d_clist, c->d_p2list,
-                    c->d_groups};
+    for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB})
+        if (st) (void)hipStreamSynchronize(st);
+    std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
+                               c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd,
+                               c->d_starts, c->d_nb};
+    for (const Batch& t : c->sets) {
+        for (void* p : t.ptrs()) ptrs.push_back(p);
+        for (hipEvent_t e : {t.evA, t.evM, t.evFree})
+            if (e) (void)hipEventDestroy(e);
+    }
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    for (hipEvent_t e : c->tev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own_stream)
+        for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB})
+            if (st) (void)hipStreamDestroy(st);
     delete c;
 }
 
@@ -554,17 +692,17 @@ int bz2mi_compress_blocks(bz2mi_ctx* c, const uint8_t* blocks, size_t stride, co
     HIPCHECK(hipSetDevice(c->device));
     int r;
     if ((r = ensure_capacity(c, (int)nblocks))) return r;
-    HIPCHECK(hipMemcpy2DAsync(c->d_blocks, c->stride, blocks, stride, std::min(stride, c->stride), nblocks,
+    HIPCHECK(hipMemcpy2DAsync(c->sets[0].d_blocks, c->stride, blocks, stride, std::min(stride, c->stride), nblocks,
                               hipMemcpyHostToDevice, c->stream));
-    HIPCHECK(hipMemcpyAsync(c->d_lens, lens, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHECK(hipMemcpyAsync(c->sets[0].d_lens, lens, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     if ((r = run_blocks(c, (int)nblocks))) return r;
     std::vector<uint64_t> bits(nblocks);
-    HIPCHECK(hipMemcpyAsync(bits.data(), c->d_pbits, nblocks * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipMemcpyAsync(bits.data(), c->sets[0].d_pbits, nblocks * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
     for (uint32_t j = 0; j < nblocks; ++j) {
         const size_t nbytes = (size_t)((bits[j] + 7) / 8);
         if (nbytes > out_stride) return fail(BZ2MI_ESPACE, "out_stride too small");
-        HIPCHECK(hipMemcpy(out + (size_t)j * out_stride, c->d_payload + (size_t)j * c->payload_words, nbytes,
+        HIPCHECK(hipMemcpy(out + (size_t)j * out_stride, c->sets[0].d_payload + (size_t)j * c->payload_words, nbytes,
                            hipMemcpyDeviceToHost));
         out_bits[j] = bits[j];
     }
@@ -583,10 +721,10 @@ int bz2mi_compress_rle1(bz2mi_ctx* c, const uint8_t* blocks, size_t stride, cons
     HIPCHECK(hipSetDevice(c->device));
     int r;
     if ((r = ensure_capacity(c, (int)nblocks))) return r;
-    HIPCHECK(hipMemcpy2DAsync(c->d_blocks, c->stride, blocks, stride, std::min(stride, c->stride), nblocks,
+    HIPCHECK(hipMemcpy2DAsync(c->sets[0].d_blocks, c->stride, blocks, stride, std::min(stride, c->stride), nblocks,
                               hipMemcpyHostToDevice, c->stream));
-    HIPCHECK(hipMemcpyAsync(c->d_lens, lens, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    HIPCHECK(hipMemcpyAsync(c->d_crc, crcs, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHECK(hipMemcpyAsync(c->sets[0].d_lens, lens, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHECK(hipMemcpyAsync(c->sets[0].d_crc, crcs, nblocks * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     if ((r = run_blocks(c, (int)nblocks))) return r;
     if ((r = assemble(c, (int)nblocks, false, out, cap, out_len))) return r;
     for (uint32_t j = 0; j < nblocks; ++j) c->stream_crc = ((c->stream_crc << 1) | (c->stream_crc >> 31)) ^ crcs[j];

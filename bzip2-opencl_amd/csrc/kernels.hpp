@@ -56,6 +56,25 @@ __global__ void huffman_kernel(const uint16_t* mtf, size_t mtf_stride, const uin
 
 __global__ void offsets_kernel(const uint64_t* bits, int nblocks, uint64_t prefix_bits, uint64_t* offs);
 
+// Stream assembly state kept on the device (pipelined compress_device).
+struct StreamDev {
+    uint64_t word_base;   // output words already final
+    uint64_t final_bits;  // stream length, set by the final batch
+    uint32_t carry;       // MSB-aligned bits of the partial word at word_base
+    uint32_t carry_bits;  // (the stream header "BZh<level>" is 32 carried bits)
+    uint32_t crc;         // combined stream CRC so far
+    uint32_t pad;
+};
+__global__ void offsets_dev_kernel(const uint64_t* bits, const uint32_t* crcs, int nblocks, StreamDev* st,
+                                   uint64_t* offs);
+__global__ void assemble_dev_kernel(const uint32_t* payload, size_t payload_words, const uint64_t* offs,
+                                    const uint32_t* crc, int nblocks, int final_, const StreamDev* st,
+                                    uint32_t* out, uint64_t cap_words);
+__global__ void volume_kernel(const uint32_t* lens, const uint32_t* mtflen, const uint64_t* pbits, int nblocks,
+                              unsigned long long* acc);
+__global__ void advance_kernel(const uint64_t* offs, int nblocks, int final_, StreamDev* st, const uint32_t* out,
+                               uint64_t cap_words);
+
 __global__ void assemble_kernel(const uint32_t* payload, size_t payload_words, const uint64_t* offs,
                                 const uint32_t* crc, int nblocks, uint64_t prefix, int prefix_bits, int final_,
                                 uint32_t stream_crc, uint32_t* out);

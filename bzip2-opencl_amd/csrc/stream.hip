@@ -117,32 +117,30 @@ __device__ int seg_bits(const Frame& f, int seg, uint64_t pos, int want, uint32_
 
 }  // namespace
 
-// One workgroup per block (plus the prefix in workgroup 0): every output word
-// is built by the segment that holds its first bit, so no word is written
-// twice and no atomics are needed.
-__global__ __launch_bounds__(256) void assemble_kernel(const uint32_t* __restrict__ payload, size_t payload_words,
-                                                       const uint64_t* __restrict__ offs,
-                                                       const uint32_t* __restrict__ crc, int nblocks,
-                                                       uint64_t prefix, int prefix_bits, int final_,
-                                                       uint32_t stream_crc, uint32_t* __restrict__ out) {
-    Frame f{payload, payload_words, offs, crc, nblocks, prefix, prefix_bits, final_, stream_crc};
-    const uint64_t end = offs[nblocks] + (final_ ? 80u : 0u);
-    // segment handled by this workgroup: blockIdx.x - 1 (workgroup 0: prefix)
+namespace {
+
+// Every output word is built by the segment that holds its first bit, so no
+// word is written twice and no atomics are needed.  Workgroup g handles
+// segment g-1 (workgroup 0: the prefix).  Words at or past cap_words are not
+// written (the caller detects the overflow from the final length).
+__device__ void assemble_body(const Frame& f, uint32_t* __restrict__ out, uint64_t cap_words) {
+    const uint64_t end = f.offs[f.nblocks] + (f.final_ ? 80u : 0u);
+    const int nblocks = f.nblocks;
     const int seg0 = (int)blockIdx.x - 1;
     if (seg0 > nblocks) return;
     uint64_t lo, hi;
     if (seg0 < 0) {
         lo = 0;
-        hi = (uint64_t)prefix_bits;
+        hi = (uint64_t)f.prefix_bits;
     } else if (seg0 < nblocks) {
-        lo = offs[seg0];
-        hi = offs[seg0 + 1];
+        lo = f.offs[seg0];
+        hi = f.offs[seg0 + 1];
     } else {
-        lo = offs[nblocks];
+        lo = f.offs[nblocks];
         hi = end;
     }
     // words whose first bit lies in [lo, hi)
-    const uint64_t w0 = (lo + 31) >> 5, w1 = (hi + 31) >> 5;
+    const uint64_t w0 = (lo + 31) >> 5, w1 = min((hi + 31) >> 5, cap_words);
     for (uint64_t w = w0 + threadIdx.x; w < w1; w += blockDim.x) {
         uint64_t pos = w << 5;
         uint32_t word = 0;
@@ -151,7 +149,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(const uint32_t* __restric
         while (got < 32 && pos < end) {
             // advance to the segment holding pos
             for (;;) {
-                uint64_t s1 = seg < 0 ? (uint64_t)prefix_bits : (seg < nblocks ? offs[seg + 1] : end);
+                uint64_t s1 = seg < 0 ? (uint64_t)f.prefix_bits : (seg < nblocks ? f.offs[seg + 1] : end);
                 if (pos < s1) break;
                 seg++;
             }
@@ -164,6 +162,103 @@ __global__ __launch_bounds__(256) void assemble_kernel(const uint32_t* __restric
         }
         out[w] = bswap32(word);
     }
+}
+
+}  // namespace
+
+// Host-driven form: prefix bits and stream CRC from the host.
+__global__ __launch_bounds__(256) void assemble_kernel(const uint32_t* __restrict__ payload, size_t payload_words,
+                                                       const uint64_t* __restrict__ offs,
+                                                       const uint32_t* __restrict__ crc, int nblocks,
+                                                       uint64_t prefix, int prefix_bits, int final_,
+                                                       uint32_t stream_crc, uint32_t* __restrict__ out) {
+    const Frame f{payload, payload_words, offs, crc, nblocks, prefix, prefix_bits, final_, stream_crc};
+    assemble_body(f, out, ~0ull);
+}
+
+// ---- device-resident stream state (pipelined compress_device): batches are
+// assembled one after another on one stream without host round trips.
+
+// offs[b] = carry_bits + sum_{b'<b} (81 + bits[b']); folds the batch's block
+// CRCs into the stream CRC: crc' = rotl(crc, nb) ^ XOR_b rotl(crc_b, nb-1-b)
+// (the sequential crc = rotl(crc, 1) ^ crc_b of OutputStream.hpp:233).
+__global__ __launch_bounds__(256) void offsets_dev_kernel(const uint64_t* __restrict__ bits,
+                                                          const uint32_t* __restrict__ crcs, int nblocks,
+                                                          StreamDev* __restrict__ st, uint64_t* __restrict__ offs) {
+    __shared__ uint64_t tmp[4];
+    __shared__ uint32_t xr[4];
+    uint64_t carry = (uint64_t)st->carry_bits;
+    uint32_t x = 0;
+    for (int base = 0; base < nblocks; base += 256) {
+        const int b = base + threadIdx.x;
+        const uint64_t v = b < nblocks ? bits[b] + (uint64_t)kHeaderBits : 0;
+        uint64_t tot;
+        const uint64_t ex = wg_excl_sum64<256>(v, tmp, &tot);
+        if (b < nblocks) {
+            offs[b] = carry + ex;
+            const uint32_t r = (uint32_t)(nblocks - 1 - b) & 31u;
+            const uint32_t cb = crcs[b];
+            x ^= r ? (cb << r) | (cb >> (32 - r)) : cb;
+        }
+        carry += tot;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x ^= (uint32_t)__shfl_xor((int)x, d);
+    if (lane_id() == 0) xr[wave_id()] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        offs[nblocks] = carry;
+        const uint32_t r = (uint32_t)nblocks & 31u, c0 = st->crc;
+        st->crc = (r ? (c0 << r) | (c0 >> (32 - r)) : c0) ^ xr[0] ^ xr[1] ^ xr[2] ^ xr[3];
+    }
+}
+
+__global__ __launch_bounds__(256) void assemble_dev_kernel(const uint32_t* __restrict__ payload, size_t payload_words,
+                                                           const uint64_t* __restrict__ offs,
+                                                           const uint32_t* __restrict__ crc, int nblocks, int final_,
+                                                           const StreamDev* __restrict__ st,
+                                                           uint32_t* __restrict__ out, uint64_t cap_words) {
+    const uint64_t base = st->word_base;
+    const Frame f{payload, payload_words, offs, crc, nblocks, (uint64_t)st->carry << 32, (int)st->carry_bits,
+                  final_, st->crc};
+    assemble_body(f, out + base, cap_words > base ? cap_words - base : 0);
+}
+
+// Volumes of a batch (RLE1 bytes, MTF symbols, payload bits) added into acc[0..2].
+__global__ __launch_bounds__(256) void volume_kernel(const uint32_t* __restrict__ lens,
+                                                     const uint32_t* __restrict__ mtflen,
+                                                     const uint64_t* __restrict__ pbits, int nblocks,
+                                                     unsigned long long* __restrict__ acc) {
+    unsigned long long a = 0, m = 0, p = 0;
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x) {
+        a += lens[b];
+        m += mtflen[b];
+        p += pbits[b];
+    }
+    if (a) atomicAdd(&acc[0], a);
+    if (m) atomicAdd(&acc[1], m);
+    if (p) atomicAdd(&acc[2], p);
+}
+
+// Move the state past the batch: whole words are final, the partial last
+// word is carried (read back from the output); the final batch records the
+// stream length instead.
+__global__ void advance_kernel(const uint64_t* __restrict__ offs, int nblocks, int final_, StreamDev* __restrict__ st,
+                               const uint32_t* __restrict__ out, uint64_t cap_words) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint64_t end = offs[nblocks] + (final_ ? 80u : 0u);
+    const uint64_t base = st->word_base;
+    if (final_) {
+        st->final_bits = base * 32 + end;
+        return;
+    }
+    const uint64_t nb = base + (end >> 5);
+    const uint32_t cb = (uint32_t)(end & 31);
+    uint32_t carry = 0;
+    if (cb && nb < cap_words) carry = bswap32(out[nb]) & (0xffffffffu << (32 - cb));
+    st->word_base = nb;
+    st->carry = carry;
+    st->carry_bits = cb;
 }
 
 }  // namespace bz2mi
