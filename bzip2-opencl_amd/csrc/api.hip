@@ -428,12 +428,12 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
     if (n > 0) {
         const dim3 g4((unsigned)((nc + 3) / 4));
         hipLaunchKernelGGL(fe_summary_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, c->d_summ);
-        hipLaunchKernelGGL(fe_runscan_kernel, dim3(1), dim3(256), 0, s, c->d_summ, nc, c->d_rsb);
+        hipLaunchKernelGGL(fe_runscan_kernel, dim3(1), dim3(kFeScanThreads), 0, s, c->d_summ, nc, c->d_rsb);
         hipLaunchKernelGGL(fe_cost_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, c->d_summ, c->d_rsb, c->d_cost,
                            c->d_ccost);
-        hipLaunchKernelGGL(fe_costscan_kernel, dim3(1), dim3(256), 0, s, c->d_ccost, nc, c->d_fc);
+        hipLaunchKernelGGL(fe_costscan_kernel, dim3(1), dim3(kFeScanThreads), 0, s, c->d_ccost, nc, c->d_fc);
         hipLaunchKernelGGL(fe_dmap_kernel, g4, dim3(256), 0, s, d_x, c->d_cost, (uint64_t)n, nc, c->d_fc, c->d_dmap);
-        hipLaunchKernelGGL(fe_chain_kernel, dim3(1), dim3(64), 0, s, d_x, c->d_cost, c->d_fc, c->d_summ, c->d_dmap,
+        hipLaunchKernelGGL(fe_chain_kernel, dim3(1), dim3(kFeChainThreads), 0, s, d_x, c->d_cost, c->d_fc, c->d_summ, c->d_dmap,
                            (uint64_t)n, nc, c->S, c->d_bnd, (uint64_t)c->fe_maxb, c->d_nb);
         HIPCHECK(hipGetLastError());
         STAGE_DONE("front-chain");

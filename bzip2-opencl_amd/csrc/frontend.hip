@@ -101,58 +101,119 @@ __global__ __launch_bounds__(256) void fe_summary_kernel(const uint8_t* __restri
     }
 }
 
-// ---- K2/K4: single-workgroup scans over chunks
+// ---- K2/K4: single-workgroup scans over chunks.  Each of the 1024 threads
+// owns kScanE consecutive chunks per tile (vector loads), the next tile's
+// loads are issued before the current tile is scanned.
+constexpr int kScanE = 8, kScanTile = kFeScanThreads * kScanE;
+
+// inclusive scan over the workgroup of per-thread values (op: max or sum);
+// returns the thread's exclusive prefix (from `carry`) and the new carry
+template <bool kMax>
+__device__ __forceinline__ uint64_t wg_scan_1024(uint64_t v, uint64_t carry, uint64_t* wt, uint64_t* total) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    uint64_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(incl, d);
+        if (lane >= d) incl = kMax ? (incl > o ? incl : o) : incl + o;
+    }
+    if (lane == 63) wt[w] = incl;
+    __syncthreads();
+    uint64_t pre = carry, all = carry;
+#pragma unroll
+    for (int q = 0; q < kFeScanThreads / 64; ++q) {
+        const uint64_t t = wt[q];
+        if (q < w) pre = kMax ? (pre > t ? pre : t) : pre + t;
+        all = kMax ? (all > t ? all : t) : all + t;
+    }
+    __syncthreads();
+    *total = all;
+    // exclusive (for sums) / inclusive-of-earlier-threads (for max) prefix
+    const uint64_t before = __shfl_up(incl, 1);
+    if (lane == 0) return pre;
+    return kMax ? (pre > before ? pre : before) : pre + before;
+}
+
 // rsb[c] = start of the run that holds byte c*CH-1 (c >= 1): an inclusive
 // max-scan of the trailing-run start of every chunk that starts a new run.
-__global__ __launch_bounds__(256) void fe_runscan_kernel(const uint4* __restrict__ summ, uint64_t nc,
-                                                         uint64_t* __restrict__ rsb) {
-    __shared__ uint64_t wtot[4];
+__global__ __launch_bounds__(kFeScanThreads) void fe_runscan_kernel(const uint4* __restrict__ summ, uint64_t nc,
+                                                                    uint64_t* __restrict__ rsb) {
+    __shared__ uint64_t wt[kFeScanThreads / 64];
     uint64_t carry = 0;
-    for (uint64_t base = 0; base < nc; base += 256) {
-        const uint64_t c = base + threadIdx.x;
-        uint64_t own = 0;
-        if (c < nc) {
-            const uint4 sm = summ[c];
-            const uint64_t c0 = c * CH;
-            if (sm.z != sm.w) {
-                own = c0 + sm.w - sm.z;  // trailing run starts inside the chunk
-            } else if (c == 0 || (sm.x & 0xff) != ((summ[c - 1].x >> 8) & 0xff)) {
-                own = c0;                // a one-run chunk that starts a new run
-            }                            // else: the run continues (own = 0)
+    auto load = [&](uint64_t c, uint4* sm) {
+#pragma unroll
+        for (int e = 0; e <= kScanE; ++e) {  // sm[0] = chunk c-1
+            const uint64_t cc = c + (uint64_t)e - 1;
+            sm[e] = (c + e >= 1 && cc < nc) ? summ[cc] : make_uint4(0, 0, 0, 0);
         }
-        uint64_t xs = own;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(xs, d);
-            if (lane_id() >= d) xs = xs > y ? xs : y;
+    };
+    uint4 cur[kScanE + 1], nxt[kScanE + 1];
+    load((uint64_t)threadIdx.x * kScanE, cur);
+    for (uint64_t base = 0; base < nc; base += kScanTile) {
+        const uint64_t c = base + (uint64_t)threadIdx.x * kScanE;
+        if (base + kScanTile < nc) load(c + kScanTile, nxt);
+        uint64_t own[kScanE], run = 0;
+#pragma unroll
+        for (int e = 0; e < kScanE; ++e) {
+            const uint64_t ce = c + e;
+            const uint4 sm = cur[e + 1];
+            uint64_t o = 0;
+            if (ce < nc) {
+                if (sm.z != sm.w) {
+                    o = ce * CH + sm.w - sm.z;  // trailing run starts inside the chunk
+                } else if (ce == 0 || (sm.x & 0xff) != ((cur[e].x >> 8) & 0xff)) {
+                    o = ce * CH;                // a one-run chunk that starts a new run
+                }                               // else: the run continues
+            }
+            run = run > o ? run : o;
+            own[e] = run;
         }
-        if (lane_id() == 63) wtot[wave_id()] = xs;
-        __syncthreads();
-        uint64_t pre = carry;
-        uint64_t all = carry;
-        for (int w = 0; w < 4; ++w) {
-            const uint64_t tw = wtot[w];
-            if (w < wave_id()) pre = pre > tw ? pre : tw;
-            all = all > tw ? all : tw;
-        }
-        const uint64_t incl = xs > pre ? xs : pre;
-        if (c < nc) rsb[c + 1] = incl;
-        carry = uniform64(all);
-        __syncthreads();
+        uint64_t all;
+        const uint64_t pre = wg_scan_1024<true>(run, carry, wt, &all);
+#pragma unroll
+        for (int e = 0; e < kScanE; ++e)
+            if (c + e < nc) rsb[c + e + 1] = pre > own[e] ? pre : own[e];
+        carry = all;
+#pragma unroll
+        for (int e = 0; e <= kScanE; ++e) cur[e] = nxt[e];
     }
     if (threadIdx.x == 0) rsb[0] = 0;
 }
 
-__global__ __launch_bounds__(256) void fe_costscan_kernel(const uint32_t* __restrict__ ccost, uint64_t nc,
-                                                          uint64_t* __restrict__ fc) {
-    __shared__ uint64_t tmp[4];
+__global__ __launch_bounds__(kFeScanThreads) void fe_costscan_kernel(const uint32_t* __restrict__ ccost, uint64_t nc,
+                                                                     uint64_t* __restrict__ fc) {
+    __shared__ uint64_t wt[kFeScanThreads / 64];
     uint64_t carry = 0;
-    for (uint64_t base = 0; base < nc; base += 256) {
-        const uint64_t c = base + threadIdx.x;
-        const uint64_t v = c < nc ? ccost[c] : 0;
-        uint64_t tot;
-        const uint64_t ex = wg_excl_sum64<256>(v, tmp, &tot);
-        if (c < nc) fc[c] = carry + ex;
-        carry += tot;
+    auto load = [&](uint64_t c, uint32_t* v) {
+        if (c + kScanE <= nc) {
+            const uint4 a = *reinterpret_cast<const uint4*>(ccost + c);
+            const uint4 b = *reinterpret_cast<const uint4*>(ccost + c + 4);
+            v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < kScanE; ++e) v[e] = c + e < nc ? ccost[c + e] : 0u;
+        }
+    };
+    static_assert(kScanE == 8, "two uint4 loads per thread");
+    uint32_t cur[kScanE], nxt[kScanE];
+    load((uint64_t)threadIdx.x * kScanE, cur);
+    for (uint64_t base = 0; base < nc; base += kScanTile) {
+        const uint64_t c = base + (uint64_t)threadIdx.x * kScanE;
+        if (base + kScanTile < nc) load(c + kScanTile, nxt);
+        uint64_t ex[kScanE], run = 0;
+#pragma unroll
+        for (int e = 0; e < kScanE; ++e) {
+            ex[e] = run;
+            run += cur[e];
+        }
+        uint64_t all;
+        const uint64_t pre = wg_scan_1024<false>(run, carry, wt, &all);
+#pragma unroll
+        for (int e = 0; e < kScanE; ++e)
+            if (c + e < nc) fc[c + e] = pre + ex[e];
+        carry = all;
+#pragma unroll
+        for (int e = 0; e < kScanE; ++e) cur[e] = nxt[e];
     }
     if (threadIdx.x == 0) fc[nc] = carry;
 }
@@ -308,67 +369,84 @@ struct FeView {
     const uint64_t* fc;
     const uint4* summ;
     uint64_t n, nc;
+    uint64_t fc_end;  // fc[nc], loaded once
 };
+
+// sum of the cost bytes in [at, at + 64) below `end` (at 16-aligned)
+__device__ __forceinline__ uint32_t cost_sum64(const uint8_t* cost, uint64_t at, uint64_t end) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t a = at + 16u * (uint64_t)j;
+        if (a < end) {
+            const uint4 v = *reinterpret_cast<const uint4*>(cost + a);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t b = a + 4u * (uint64_t)q;
+                uint32_t d = w[q];
+                if (b + 4 > end) d = b >= end ? 0u : d & ((1u << (8 * (uint32_t)(end - b))) - 1u);
+                s = __builtin_amdgcn_sad_u8(d, 0u, s);
+            }
+        }
+    }
+    return s;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return (uint64_t)hi << 32 | lo;
+}
 
 // Fg(i) by one wave: chunk prefix + in-chunk sum (all lanes return it)
 __device__ uint64_t fg_at(const FeView& f, uint64_t i) {
-    if (i >= f.n) return f.fc[f.nc];
+    if (i >= f.n) return f.fc_end;
     const uint64_t c = i / CH, c0 = c * CH;
-    const int lane = lane_id();
-    uint32_t s = 0;
-    for (uint64_t j = c0 + lane; j < i; j += 64) s += f.cost[j];
-    s = wave_sum(s);
+    const uint32_t s = wave_sum(cost_sum64(f.cost, c0 + 64u * (uint64_t)lane_id(), i));
     return f.fc[c] + s;
 }
 
-// Ginv(y) = min { i : Fg(i) > y } by one wave (binary search over chunks,
-// then an in-chunk scan); returns n if none.
+// Ginv(y) = min { i : Fg(i) > y } by one wave: a 65-ary search over the
+// chunk prefixes (each lane probes one point per level), lane sums over the
+// chunk, then a scan of the 64 bytes that hold the crossing; n if none.
 __device__ uint64_t ginv(const FeView& f, uint64_t y) {
-    if (f.fc[f.nc] <= y) return f.n;
-    // largest c with fc[c] <= y
+    if (f.fc_end <= y) return f.n;
+    const int lane = lane_id();
     uint64_t lo = 0, hi = f.nc;  // fc[lo] <= y < fc[hi]
     while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) / 2;
-        if (f.fc[mid] <= y) lo = mid;
-        else hi = mid;
+        const uint64_t q = lo + ((hi - lo) * (uint64_t)(lane + 1)) / 65u;
+        const int cnt = __popcll(__ballot(f.fc[q] <= y));  // fc is monotone: a prefix of lanes
+        const uint64_t nlo = cnt ? readlane64(q, cnt - 1) : lo;
+        const uint64_t nhi = cnt < 64 ? readlane64(q, cnt) : hi;
+        lo = nlo;
+        hi = nhi;
     }
-    const uint64_t c0 = lo * CH;
-    const int lane = lane_id();
-    const uint64_t at = c0 + (uint64_t)lane * 64;
-    uint32_t ls = 0;
-    for (int q = 0; q < 64; ++q)
-        if (at + q < f.n) ls += f.cost[at + q];
+    const uint64_t c0 = lo * CH, cend = min(f.n, c0 + CH);
+    const uint64_t at = c0 + 64u * (uint64_t)lane;
+    const uint32_t ls = cost_sum64(f.cost, at, cend);
     const uint32_t incl = wave_incl_sum(ls);
-    const uint64_t base = f.fc[lo] + (incl - ls);
-    // lane whose range holds the first i with Fg(i) > y: Fg(i) = base + prefix up to i
-    // i in (at, at+64]: Fg(at+q+1) = base + sum_{<=q}
-    const uint64_t target = y;
-    uint64_t found = ~0ull;
-    uint64_t run = base;
-    for (int q = 0; q < 64; ++q) {
-        if (at + q >= f.n) break;
-        run += f.cost[at + q];
-        if (run > target) {
-            found = at + q + 1;
-            break;
-        }
-    }
-    // smallest found across lanes
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t o = __shfl_xor(found, d);
-        found = o < found ? o : found;
-    }
-    return found == ~0ull ? f.n : found;
+    const uint64_t over = __ballot(f.fc[lo] + incl > y);
+    if (!over) return f.n;
+    const int L = __ffsll((long long)over) - 1;
+    const uint64_t baseL = f.fc[lo] + (uint32_t)__builtin_amdgcn_readlane((int)(incl - ls), L);
+    const uint64_t atL = c0 + 64u * (uint64_t)L;
+    const uint32_t cb = atL + lane < f.n ? f.cost[atL + lane] : 0u;
+    const uint64_t hit = __ballot(baseL + wave_incl_sum(cb) > y);
+    return hit ? atL + (uint64_t)__ffsll((long long)hit) : f.n;
 }
 
-// first index > p whose byte differs from x[p] (or n)
+// first index > p whose byte differs from x[p] (or n): whole chunks that are
+// one run are skipped by their summaries, otherwise each lane compares 16
+// bytes (four aligned dwords) per pass
 __device__ uint64_t run_end(const FeView& f, uint64_t p) {
     const uint32_t v = f.x[p];
+    const uint32_t vv = v * 0x01010101u;
     uint64_t at = p + 1;
     const int lane = lane_id();
+    const uint64_t mis = (uint64_t)(reinterpret_cast<uintptr_t>(f.x) & 3u);
     for (;;) {
         if (at >= f.n) return f.n;
-        // skip whole chunks that are one run of v
         const uint64_t c = at / CH;
         if (at == c * CH && c < f.nc) {
             const uint4 s = f.summ[c];
@@ -377,132 +455,323 @@ __device__ uint64_t run_end(const FeView& f, uint64_t p) {
                 continue;
             }
         }
-        const uint64_t i = at + lane;
-        const bool diff = i >= f.n || f.x[i] != v;
-        const uint64_t m = __ballot(diff);
-        if (m) return at + (uint64_t)(__ffsll((long long)m) - 1);
-        at += 64;
+        // dword-aligned base (as an index relative to x, may be up to 3 below at)
+        const uint64_t base = ((at + mis) & ~3ull) - mis;
+        uint32_t off = 64;
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+            const uint64_t b = base + 4u * (uint64_t)(lane * 4 + j);
+            uint32_t d = 0xffffffffu;
+            if (b + 4 <= at) {
+                d = 0;  // wholly before at
+            } else if (b < f.n) {
+                d = *reinterpret_cast<const uint32_t*>(f.x + b) ^ vv;
+                if (b < at) d &= ~0u << (8 * (uint32_t)(at - b));
+            }
+            if (d) off = 4u * j + (__builtin_ctz(d) >> 3);
+        }
+        const uint64_t m = __ballot(off < 64);
+        if (m) {
+            const int L = __ffsll((long long)m) - 1;
+            const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)off, L);
+            const uint64_t e = base + 16u * (uint64_t)L + o;
+            return e < f.n ? e : f.n;
+        }
+        at = base + 1024;
     }
 }
 
 }  // namespace
 
-// ---- K6: the block chain (one wave).  bnd[k] is the start of block k+1,
+// ---- K6: the block chain (one workgroup).  bnd[k] is the start of block k+1,
 // either as a target y (bit 63 clear: start = Ginv(y)) or as an explicit
 // position (bit 63 set).  *nb_out = number of blocks.
-__global__ __launch_bounds__(64) void fe_chain_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
+__global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
                                                       const uint64_t* __restrict__ fc, const uint4* __restrict__ summ,
                                                       const uint8_t* __restrict__ dmap, uint64_t n, uint64_t nc, int S,
                                                       uint64_t* __restrict__ bnd, uint64_t max_bnd,
                                                       uint64_t* __restrict__ nb_out) {
-    FeView f{x, cost, fc, summ, n, nc};
-    const int lane = lane_id();
+    FeView f{x, cost, fc, summ, n, nc, uniform64(fc[nc])};
     if (n == 0) {
-        if (lane == 0) *nb_out = 0;
+        if (threadIdx.x == 0) *nb_out = 0;
         return;
     }
     // Ytot: targets y >= Fg(n-1) have no boundary inside the input
     const uint64_t ytot = fc[nc] - cost[n - 1];
     const uint64_t lim = (uint64_t)(S - 6);
     const uint32_t jstar = (uint32_t)((S - 6) / 5 + 1);
+    // Case-A steps advance y by D + S-6 (D < 16).  A round covers the next
+    // kStepsR steps: step m gets a 256-byte window of the D map around its
+    // predicted position (running mean of D) and all waves turn every window
+    // byte into a transition (offset of the next start in step m+1's window,
+    // or a terminal code), then compose them into 8-step jumps.  Wave 0 then
+    // chases the chain through the jumps (one LDS read per 8 blocks), takes
+    // single steps near terminals, runs the mid-run slow path itself and
+    // resumes the chase when the chain comes back into the windows.  The
+    // offsets of jumped-over steps are replayed in parallel afterwards and
+    // the block starts written out by all threads.
+    constexpr int kStepsR = 128, kWin = 256, kJ = 16, kGroups = kStepsR / kJ;
+    constexpr uint32_t kOut = 0x100, kMidRun = 0x200, kEnd = 0x300;  // kOut | D&15
+    constexpr uint16_t kStop = 0xffff, kDirect = 0xffff;
+    __shared__ uint16_t trans[kStepsR * kWin];
+    __shared__ uint16_t jmp[kGroups * kWin];
+    __shared__ uint16_t walk[kStepsR];  // offset of step m, or kDirect (bnd written by the slow path)
+    __shared__ uint32_t jumped[kGroups];
+    __shared__ uint64_t ctl[4];  // next round's y (or ~0: the chain ended), k after the round, steps
+    const int tid = threadIdx.x;
+    // chain state (wave 0; uniform)
     uint64_t k = 0;
-    // state: either a target y (case A block) or an explicit mid-run start p
-    bool have_y = true;
-    uint64_t y = lim;   // block 0 starts at 0 (a run start), Fg(1) = 0
-    uint64_t p = 0;
-    // Case-A steps advance y by D + S-6 (D < 16, typically near its running
-    // mean).  One round of loads fetches, for each of the next 64 steps, a
-    // 32-byte window of D bytes around the predicted position (lane m: step
-    // m, 9 aligned dwords); the steps are then followed with readlanes until
-    // one lands outside its window, which starts the next round.
-    uint32_t dsum = 0, dcnt = 0;
-    bool finished = false;
-    int nwin = 0;
+    uint64_t y = lim;  // block 0 starts at 0 (a run start), Fg(1) = 0
+    uint64_t dsum = 0, dcnt = 0;  // (wave 0)
+    uint64_t dfp = 8ull << 16;    // mean D, 16.16, for the window predictions
+    [[maybe_unused]] int nwin = 0, nslow = 0;
+#ifdef BZ2MI_PHASES
+#define FE_NOW() wall_clock64()
+#else
+#define FE_NOW() 0ull
+#endif
+    unsigned long long t_tab = 0, t_ch = 0, t_bnd = 0, t_slow = 0, n_out = 0, n_mid = 0;
+    constexpr uint64_t kEnded = ~0ull;
     for (;;) {
-        if (k + 1 >= max_bnd) break;
-        if (have_y) {
-            if (y >= ytot) break;  // last block
-            BZ2MI_PHASE(g_fe_phase, nwin < 16 ? nwin : 15, nwin < 16);
-            nwin++;
-            const uint64_t ybase = y;
-            const uint32_t dg = dcnt ? dsum / dcnt : 1u;  // predicted mean D
-            // window start of step m: ybase + m (lim + dg) - 16, not before step m's minimum
-            const uint64_t pm = ybase + (uint64_t)lane * (lim + dg);
-            const uint64_t lo_m = ybase + (uint64_t)lane * lim;
-            const uint64_t wstart = pm >= lo_m + 16 ? pm - 16 : lo_m;
-            const uint64_t abase = wstart & ~3ull;
-            uint32_t w[9];
+        if (k + 1 >= max_bnd || y >= ytot) break;  // (y == kEnded too)
+        const unsigned long long tr = FE_NOW();
+        BZ2MI_PHASE(g_fe_phase, nwin < 6 ? nwin : 5, nwin < 6);
+        nwin++;
+        const uint64_t ybase = y, k0 = k;
+        // window of step m: 16-aligned, from 128 below the prediction but
+        // not below step m's minimum position ybase + m (S-6)
+        auto wstart_of = [&](uint64_t m) -> uint64_t {
+            const uint64_t lo_m = ybase + m * lim;
+            const uint64_t pm = lo_m + ((m * dfp) >> 16);
+            return (pm >= lo_m + 128 ? pm - 128 : lo_m) & ~15ull;
+        };
+        static_assert(kStepsR * (kWin / 16) % kFeChainThreads == 0, "table items per thread");
 #pragma unroll
-            for (int q = 0; q < 9; ++q) {
-                const uint64_t ad = abase + 4u * q;
-                w[q] = ad + 4 <= ytot ? *reinterpret_cast<const uint32_t*>(dmap + ad) : 0u;
+        for (int it = tid; it < kStepsR * (kWin / 16); it += kFeChainThreads) {
+            const int m = it >> 4, c = it & 15;
+            const uint64_t ws = wstart_of((uint64_t)m), wsn = wstart_of((uint64_t)m + 1);
+            const uint64_t y0 = ws + 16u * (uint64_t)c;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (y0 < ytot) v = *reinterpret_cast<const uint4*>(dmap + y0);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            uint32_t packed[8];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint64_t yy = y0 + (uint64_t)q;
+                const uint32_t d = (w[q >> 2] >> (8 * (q & 3))) & 0xffu;
+                uint32_t t;
+                if (yy >= ytot) {
+                    t = kEnd;
+                } else if (!(d & 16u)) {
+                    t = kMidRun;
+                } else {
+                    const uint64_t yn = yy + (d & 15u) + lim;
+                    t = (m + 1 < kStepsR && yn >= wsn && yn < wsn + kWin) ? (uint32_t)(yn - wsn) : (kOut | (d & 15u));
+                }
+                if (q & 1) packed[q >> 1] |= t << 16;
+                else packed[q >> 1] = t;
             }
-            for (int m = 0; m < 64; ++m) {
-                if (y >= ytot || k + 1 >= max_bnd) {
-                    finished = true;
+            uint4* dst = reinterpret_cast<uint4*>(trans + m * kWin + 16 * c);
+            dst[0] = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+            dst[1] = make_uint4(packed[4], packed[5], packed[6], packed[7]);
+        }
+        if (tid < kGroups) jumped[tid] = 0;
+        __syncthreads();
+        // jumps: group g covers the kJ steps from step kJ g (the last group
+        // kJ - 1: step kStepsR - 1 always leaves the windows); kStop if a
+        // terminal lies inside
+        static_assert(kGroups * kWin % kFeChainThreads == 0, "jump items per thread");
+        {
+            constexpr int kPer = kGroups * kWin / kFeChainThreads;
+            uint32_t o[kPer];
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) o[e] = (uint32_t)((tid + e * kFeChainThreads) & (kWin - 1));
+#pragma unroll
+            for (int i = 0; i < kJ; ++i) {
+#pragma unroll
+                for (int e = 0; e < kPer; ++e) {
+                    const int g = (tid + e * kFeChainThreads) / kWin;
+                    if (o[e] < (uint32_t)kWin && g * kJ + i < kStepsR - 1) o[e] = trans[(g * kJ + i) * kWin + (int)o[e]];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) jmp[tid + e * kFeChainThreads] = o[e] < (uint32_t)kWin ? (uint16_t)o[e] : kStop;
+        }
+        __syncthreads();
+        const unsigned long long t1 = FE_NOW();
+        t_tab += t1 - tr;
+        if (tid < 64) {
+            int m = 0;
+            uint32_t o = (uint32_t)(y - wstart_of(0));
+            bool clean = true;
+            auto direct = [&](uint64_t v) {  // a block start found by the slow path
+                if (tid == 0) {
+                    bnd[k] = v;
+                    if (m < kStepsR) walk[m] = kDirect;
+                }
+                m++;
+                k++;
+            };
+            for (;;) {
+                if ((m & (kJ - 1)) == 0) {
+                    const int len = m + kJ < kStepsR ? kJ : kJ - 1;
+                    if (k + (uint64_t)len < max_bnd) {
+                        const uint32_t j = (uint32_t)__builtin_amdgcn_readfirstlane((int)jmp[(m / kJ) * kWin + (int)o]);
+                        if (j != kStop) {
+                            if (tid == 0) {
+                                walk[m] = (uint16_t)o;
+                                jumped[m / kJ] = 1;
+                            }
+                            o = j;
+                            m += len;
+                            k += (uint64_t)len;
+                            continue;
+                        }
+                    }
+                }
+                if (k + 1 >= max_bnd) {
+                    y = kEnded;
                     break;
                 }
-                const uint64_t ws = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)wstart, m) |
-                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wstart >> 32), m) << 32);
-                if (y < ws || y >= ws + 32) break;  // outside the window: new round
-                const uint32_t rel = (uint32_t)(y - (ws & ~3ull));
-                const uint32_t qi = rel >> 2;
-                uint32_t sel = w[0];
-#pragma unroll
-                for (int q = 1; q < 9; ++q) sel = qi == (uint32_t)q ? w[q] : sel;
-                const uint32_t d = ((uint32_t)__builtin_amdgcn_readlane((int)sel, m) >> ((rel & 3u) * 8u)) & 0xffu;
-                if (lane == 0) bnd[k] = y;
-                k++;
-                if (d & 16u) {  // next block starts at a run start
-                    y = y + (d & 15u) + lim;
-                    dsum += d & 15u;
-                    dcnt++;
+                const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)trans[m * kWin + (int)o]);
+                if (t < (uint32_t)kWin) {
+                    if (tid == 0) walk[m] = (uint16_t)o;
+                    o = t;
+                    m++;
+                    k++;
                     continue;
                 }
-                p = ginv(f, y);  // next block starts inside a run
-                have_y = false;
+                // a terminal at step m
+                y = uniform64(wstart_of((uint64_t)m) + o);
+                if (t == kEnd) {
+                    y = kEnded;  // y >= ytot: no boundary inside the input
+                    break;
+                }
+                if (tid == 0) walk[m] = (uint16_t)o;  // the block at y itself
+                m++;
+                k++;
+                if ((t & ~15u) == kOut) {  // next start outside the windows: new round from it
+                    if (clean) {
+                        dsum += y - ybase - (uint64_t)(m - 1) * lim;
+                        dcnt += (uint64_t)(m - 1);
+                    }
+                    y = uniform64(y + (uint64_t)(t & 15u) + lim);
+                    n_out++;
+                    break;
+                }
+                // the next block starts inside a run: the slow path, block by
+                // block, until the chain is back on a run start (have y)
+                n_mid++;
+                const unsigned long long ts = FE_NOW();
+                if (clean) {
+                    dsum += y - ybase - (uint64_t)(m - 1) * lim;
+                    dcnt += (uint64_t)(m - 1);
+                }
+                clean = false;
+                uint64_t p = ginv(f, y);
+                bool have_y = false;
+                while (!have_y) {
+                    if (k + 1 >= max_bnd) break;
+                    nslow++;
+                    // block starting at p, mid-run: its first run is [p, e)
+                    const uint64_t e = run_end(f, p);
+                    const uint64_t Lr = e - p;
+                    if ((uint64_t)jstar * 255u <= Lr) {
+                        const uint64_t E = p + (uint64_t)jstar * 255u;
+                        if (E >= n) break;
+                        direct(E | (1ull << 63));
+                        if (E < e) {
+                            p = E;  // still inside the run
+                            continue;
+                        }
+                        // E == e: a run start
+                        y = fg_at(f, E + 1) + lim;
+                        have_y = true;
+                        continue;
+                    }
+                    if (e >= n) break;  // the run reaches the end: last block
+                    const uint64_t tot = 5ull * (Lr / 255) + piece_cost((uint32_t)(Lr % 255));
+                    if (tot > lim) {
+                        const uint64_t E = e + 1;
+                        if (E >= n) break;
+                        direct(E | (1ull << 63));
+                        if (f.x[E] != f.x[E - 1]) {
+                            y = fg_at(f, E + 1) + lim;
+                            have_y = true;
+                        } else {
+                            p = E;
+                        }
+                        continue;
+                    }
+                    // continue in unsplit coordinates after the run
+                    y = fg_at(f, e + 1) - tot + lim;
+                    have_y = true;
+                }
+                t_slow += FE_NOW() - ts;
+                if (!have_y) {
+                    y = kEnded;
+                    break;
+                }
+                // back in the windows?  then the chase goes on
+                if (m < kStepsR && y < ytot) {
+                    const uint64_t ws = wstart_of((uint64_t)m);
+                    if (y >= ws && y < ws + kWin) {
+                        o = (uint32_t)(y - ws);
+                        continue;
+                    }
+                }
                 break;
             }
-            if (finished) break;
-            continue;
-        }
-        // block starting at p, mid-run: its first run is [p, e)
-        const uint64_t e = run_end(f, p);
-        const uint64_t Lr = e - p;
-        if ((uint64_t)jstar * 255u <= Lr) {
-            const uint64_t E = p + (uint64_t)jstar * 255u;
-            if (E >= n) break;
-            if (lane == 0) bnd[k] = E | (1ull << 63);
-            k++;
-            if (E < e) {
-                p = E;  // still inside the run
-                continue;
+            if (tid == 0) {
+                ctl[0] = y;
+                ctl[1] = k;
+                ctl[2] = (uint64_t)m;
+                ctl[3] = dcnt ? (uint64_t)((float)dsum / (float)dcnt * 65536.0f) : dfp;
             }
-            // E == e: a run start
-            y = fg_at(f, E + 1) + lim;
-            have_y = true;
-            continue;
         }
-        if (e >= n) break;  // the run reaches the end: last block
-        const uint64_t tot = 5ull * (Lr / 255) + piece_cost((uint32_t)(Lr % 255));
-        if (tot > lim) {
-            const uint64_t E = e + 1;
-            if (E >= n) break;
-            if (lane == 0) bnd[k] = E | (1ull << 63);
-            k++;
-            if (f.x[E] != f.x[E - 1]) {
-                y = fg_at(f, E + 1) + lim;
-                have_y = true;
-            } else {
-                p = E;
+        __syncthreads();
+        const unsigned long long t2 = FE_NOW();
+        t_ch += t2 - t1;
+        y = ctl[0];
+        k = ctl[1];
+        const int msteps = min((int)ctl[2], kStepsR);
+        const uint64_t dfp_next = ctl[3];
+        // replay the jumped-over steps (one thread per group)
+        if (tid < kGroups && jumped[tid]) {
+            uint32_t o = walk[tid * kJ];
+            const int len = tid * kJ + kJ < kStepsR ? kJ : kJ - 1;
+            for (int i = 1; i < len; ++i) {
+                o = trans[(tid * kJ + i - 1) * kWin + (int)o];
+                walk[tid * kJ + i] = (uint16_t)o;
             }
-            continue;
         }
-        // continue in unsplit coordinates after the run
-        y = fg_at(f, e + 1) - tot + lim;
-        have_y = true;
+        __syncthreads();
+        for (int j = tid; j < msteps; j += kFeChainThreads) {
+            const uint16_t o = walk[j];
+            if (o != kDirect) bnd[k0 + j] = wstart_of((uint64_t)j) + o;
+        }
+        __syncthreads();  // trans/walk are rewritten by the next round
+        dfp = dfp_next;
+        t_bnd += FE_NOW() - t2;
     }
-    if (lane == 0) *nb_out = k + 1;
+#ifdef BZ2MI_PHASES
+    if (threadIdx.x == 0) {
+        g_fe_phase[6] = t_tab;
+        g_fe_phase[7] = t_ch;
+        g_fe_phase[8] = t_bnd;
+        g_fe_phase[9] = t_slow;
+        g_fe_phase[10] = n_out;
+        g_fe_phase[11] = n_mid;
+        g_fe_phase[12] = (unsigned long long)nwin;
+        g_fe_phase[13] = k;
+        g_fe_phase[14] = (unsigned long long)nslow;
+        g_fe_phase[15] = wall_clock64();
+    }
+#else
+    (void)nslow;
+    (void)t_tab, (void)t_ch, (void)t_bnd, (void)t_slow, (void)n_out, (void)n_mid;
+#endif
+    if (threadIdx.x == 0) *nb_out = k + 1;
 }
 
 // ---- K7: boundary targets -> positions; starts[0] = 0, starts[nb] = n
@@ -510,7 +779,7 @@ __global__ __launch_bounds__(256) void fe_resolve_kernel(const uint8_t* __restri
                                                          const uint64_t* __restrict__ fc, const uint4* __restrict__ summ,
                                                          uint64_t n, uint64_t nc, const uint64_t* __restrict__ bnd,
                                                          const uint64_t* __restrict__ nb_in, uint64_t* __restrict__ starts) {
-    FeView f{x, cost, fc, summ, n, nc};
+    FeView f{x, cost, fc, summ, n, nc, uniform64(fc[nc])};
     const uint64_t nb = *nb_in;
     const uint64_t k = (uint64_t)blockIdx.x * 4 + wave_id();
     if (k == 0 && lane_id() == 0) {

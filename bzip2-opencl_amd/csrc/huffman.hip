@@ -400,7 +400,7 @@ __global__ __launch_bounds__(256) void huffman_kernel(
     const int nsel = (m + kGroupRun - 1) / kGroupRun;
     const uint16_t* X = mtf + (size_t)b * mtf_stride;
     uint32_t* out = payload + (size_t)b * payload_words;
-    const bool stamp = b == nblocks / 2;
+    [[maybe_unused]] const bool stamp = b == nblocks / 2;
     BZ2MI_PHASE(g_huf_phase, 0, stamp);
 
     // ---- seeds: symbol ranges of roughly equal frequency per table (wave 0,

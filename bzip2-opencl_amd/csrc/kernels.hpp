@@ -82,12 +82,14 @@ __global__ void assemble_kernel(const uint32_t* payload, size_t payload_words, c
 // Device RLE1 front end (frontend.hip); chunks are 4096 bytes.
 constexpr int kFeChunk = 4096;
 __global__ void fe_summary_kernel(const uint8_t* x, uint64_t n, uint64_t nc, uint4* summ);
+constexpr int kFeScanThreads = 1024;  // one workgroup
 __global__ void fe_runscan_kernel(const uint4* summ, uint64_t nc, uint64_t* rsb);
 __global__ void fe_cost_kernel(const uint8_t* x, uint64_t n, uint64_t nc, const uint4* summ, const uint64_t* rsb,
                                uint8_t* cost, uint32_t* ccost);
 __global__ void fe_costscan_kernel(const uint32_t* ccost, uint64_t nc, uint64_t* fc);
 __global__ void fe_dmap_kernel(const uint8_t* x, const uint8_t* cost, uint64_t n, uint64_t nc, const uint64_t* fc,
                                uint8_t* dmap);
+constexpr int kFeChainThreads = 1024;  // one workgroup
 __global__ void fe_chain_kernel(const uint8_t* x, const uint8_t* cost, const uint64_t* fc, const uint4* summ,
                                 const uint8_t* dmap, uint64_t n, uint64_t nc, int S, uint64_t* bnd, uint64_t max_bnd,
                                 uint64_t* nb_out);

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
     // per block: 64 initial MTF lists (256 bytes each) in global scratch
     // (the recency lists live in LDS)
     uint16_t* out = mtf_out + (size_t)b * mtf_stride;
-    const bool stamp = b == nblocks / 2;
+    [[maybe_unused]] const bool stamp = b == nblocks / 2;
     BZ2MI_PHASE(g_mtf_phase, 0, stamp);
 
     int L = (n + NL - 1) / NL;

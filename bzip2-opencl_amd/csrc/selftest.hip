@@ -38,10 +38,10 @@ __global__ __launch_bounds__(64) void selftest_kernel(uint32_t* bad) {
 int run_selftest(uint32_t* host_bad, int n) {
     uint32_t* d = nullptr;
     if (hipMalloc(&d, 16 * sizeof(uint32_t)) != hipSuccess) return -1;
-    hipMemset(d, 0, 16 * sizeof(uint32_t));
+    (void)hipMemset(d, 0, 16 * sizeof(uint32_t));
     hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(64), 0, 0, d);
     const hipError_t e = hipMemcpy(host_bad, d, sizeof(uint32_t) * (n < 16 ? n : 16), hipMemcpyDeviceToHost);
-    hipFree(d);
+    (void)hipFree(d);
     return e == hipSuccess ? 10 : -1;
 }
 
