@@ -69,8 +69,6 @@ struct Batch {
     uint32_t* d_p2list = nullptr;
     bz2mi::BwtSeg* d_groups = nullptr;
     // MTF / Huffman
-    uint8_t* d_ranks = nullptr;
-    uint8_t* d_rec = nullptr;
     uint16_t* d_mtf = nullptr;
     uint32_t* d_mtflen = nullptr;
     uint32_t* d_alpha = nullptr;
@@ -85,7 +83,7 @@ struct Batch {
 
     std::vector<void*> ptrs() const {
         return {d_blocks, d_lens, d_crc, d_bwt, d_orig, d_sa, d_bq, d_bcnt, d_large, d_nlarge, d_ngroups, d_clist,
-                d_p2list, d_groups, d_ranks, d_rec, d_mtf, d_mtflen, d_alpha, d_hist, d_present, d_seed, d_payload,
+                d_p2list, d_groups, d_mtf, d_mtflen, d_alpha, d_hist, d_present, d_seed, d_payload,
                 d_pbits, d_offs};
     }
 };
@@ -185,8 +183,6 @@ int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks) {
     if ((r = dalloc(&t.d_clist, B))) return r;
     if ((r = dalloc(&t.d_p2list, B))) return r;
     if ((r = dalloc(&t.d_groups, B * bz2mi::bwt_group_stride(c->stride)))) return r;
-    if ((r = dalloc(&t.d_ranks, B * c->stride))) return r;
-    if ((r = dalloc(&t.d_rec, B * 64 * 512))) return r;
     if ((r = dalloc(&t.d_mtf, B * c->mtf_stride))) return r;
     if ((r = dalloc(&t.d_mtflen, B))) return r;
     if ((r = dalloc(&t.d_alpha, B))) return r;
@@ -236,7 +232,7 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     const int slots = std::min(nb, c->bwt_slots);
     hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
                        t.d_bwt, t.d_orig, t.d_bq, t.d_bcnt, t.d_large, t.d_nlarge, t.d_ngroups, t.d_clist,
-                       t.d_bcnt + 1);
+                       t.d_bcnt + 1, t.d_present);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");
     hipLaunchKernelGGL(bwt_small_kernel, dim3(c->cus * 8), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, t.d_sa,
@@ -258,8 +254,8 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
 
 int stage_mtf(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     using namespace bz2mi;
-    hipLaunchKernelGGL(mtf_kernel, dim3(nb), dim3(64), 0, s, t.d_bwt, c->stride, t.d_lens, nb, t.d_ranks, t.d_rec,
-                       t.d_mtf, c->mtf_stride, t.d_mtflen, t.d_alpha, t.d_hist, t.d_present);
+    hipLaunchKernelGGL(mtf_kernel, dim3(nb), dim3(64), 0, s, t.d_bwt, c->stride, t.d_lens, nb, t.d_present, t.d_mtf,
+                       c->mtf_stride, t.d_mtflen, t.d_alpha, t.d_hist);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("mtf");
     return BZ2MI_OK;

@@ -768,7 +768,8 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
                                                          uint32_t* __restrict__ orig_out, uint64_t* __restrict__ queue,
                                                          uint32_t* __restrict__ qcount, Seg* __restrict__ large_all,
                                                          uint32_t* __restrict__ nlarge, uint32_t* __restrict__ ngroups,
-                                                         uint32_t* __restrict__ clist, uint32_t* __restrict__ ccount) {
+                                                         uint32_t* __restrict__ clist, uint32_t* __restrict__ ccount,
+                                                         uint32_t* __restrict__ present_out) {
     __shared__ BwtShared sh;
     const int b = blockIdx.x;
     if (b >= nblocks) return;
@@ -783,11 +784,19 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
             orig_out[b] = 0;
             nlarge[b] = 0;
         }
+        if (t < 8) present_out[(size_t)b * 8 + t] = (n == 1 && (T[0] >> 5) == t) ? 1u << (T[0] & 31) : 0u;
         return;
     }
     uint32_t* sa = sa_all + (size_t)b * stride;
     uint32_t c, ex;
     count_sort_first(T, n, sa, sh, &c, &ex);
+    {  // symbols in use (the MTF symbol map): bit t of the 256-bit set
+        const uint64_t m = __ballot(c != 0);
+        if (lane_id() == 0) {
+            present_out[(size_t)b * 8 + 2 * wave_id()] = (uint32_t)m;
+            present_out[(size_t)b * 8 + 2 * wave_id() + 1] = (uint32_t)(m >> 32);
+        }
+    }
     if (c == 1) {
         const uint32_t i = sa[ex];
         out[ex] = bwt_byte(T, n, i);

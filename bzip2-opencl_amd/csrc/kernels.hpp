@@ -19,7 +19,7 @@ struct BwtSeg {
 __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                                   uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint64_t* queue,
                                   uint32_t* qcount, BwtSeg* large_all, uint32_t* nlarge, uint32_t* ngroups,
-                                  uint32_t* clist, uint32_t* ccount);
+                                  uint32_t* clist, uint32_t* ccount, uint32_t* present_out);
 __global__ void bwt_small_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                  uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* queue,
                                  const uint32_t* qcount, BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list,
@@ -36,9 +36,10 @@ __global__ void bwt_double_kernel(const uint8_t* blocks, size_t stride, const ui
 // per-block group list capacity (BwtSeg entries) for a block stride
 __host__ __device__ inline size_t bwt_group_stride(size_t stride) { return stride / 2 + 2; }
 
-__global__ void mtf_kernel(const uint8_t* bwt, size_t stride, const uint32_t* lens, int nblocks, uint8_t* ranks,
-                           uint8_t* rec, uint16_t* mtf_out, size_t mtf_stride, uint32_t* mtf_len,
-                           uint32_t* alpha_out, uint32_t* hist_out, uint32_t* present_out);
+// MTF + RLE2, one wave per block; `present` (8 words per block) comes from bwt_bucket_kernel
+__global__ void mtf_kernel(const uint8_t* bwt, size_t stride, const uint32_t* lens, int nblocks, const uint32_t* present,
+                           uint16_t* mtf_out, size_t mtf_stride, uint32_t* mtf_len, uint32_t* alpha_out,
+                           uint32_t* hist_out);
 
 __global__ void seed_kernel(const uint32_t* hist, uint32_t* seed, uint32_t* state, int nblocks, int p,
                             uint64_t first_block);
