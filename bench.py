@@ -32,6 +32,16 @@ METRIC = "compress MB/s at -9 (900KB blocks), bit-exact .bz2; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
+WORKLOADS = {
+    "random": "C2: {mib} MiB random bytes per GPU (torch Philox, seed 0x5EED0001+rank) resident in HBM -> "
+              "one .bz2 stream per GPU",
+    "text": "C3: {mib} MiB seeded word-Markov text per GPU (synth.text_bytes, seed 0x5EED0002+rank; enwik9 "
+            "stand-in) resident in HBM -> one .bz2 stream per GPU",
+    "mixed": "C4: {mib} MiB mixed-entropy stream per GPU (synth.mixed_bytes, seed 0x5EED0003+rank, 64 MiB "
+             "segments of random/text/runs/ACGT) resident in HBM -> one .bz2 stream per GPU",
+}
+
+
 def ensure_built():
     so = os.path.join(PKG, "bz2mi", "libbz2mi.so")
     if not os.path.exists(so):
@@ -91,6 +101,9 @@ def main():
     ap.add_argument("--cpu-sample-mib", type=int, default=96)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--data", choices=["random", "text", "mixed"], default="random",
+                    help="random = C2 (the bench line); text = C3 stand-in (seeded word Markov text, enwik9 is "
+                         "not available offline); mixed = C4 (rotating random/text/runs/ACGT segments)")
     args = ap.parse_args()
 
     import torch
@@ -111,7 +124,12 @@ def main():
     dev = torch.device("cuda", local)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED0001 + rank)
-    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+    if args.data == "random":
+        x = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+    else:
+        from bz2mi import synth
+        gen = synth.text_bytes if args.data == "text" else synth.mixed_bytes
+        x = torch.from_numpy(gen(n, (synth.SEED_TEXT if args.data == "text" else synth.SEED_MIXED) + rank)).to(dev)
     cap = bz2mi.compress_bound(n, args.level, args.unit)
     out = torch.empty(cap, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -187,8 +205,7 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"C2: {args.mib} MiB random bytes per GPU (torch Philox, seed 0x5EED0001+rank) "
-                               f"resident in HBM -> one .bz2 stream per GPU",
+        "config": {"workload": WORKLOADS[args.data].format(mib=args.mib),
                    "level": args.level, "block_size": args.level * args.unit, "parallel_blocks": args.parallel,
                    "input_bytes_per_gpu": n, "output_bytes": int(out_len), "ratio": round(out_len / n, 5),
                    "blocks": nb, "parallelism": f"dp{world} (independent streams)", "decode_check": verified},

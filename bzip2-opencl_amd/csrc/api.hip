@@ -57,15 +57,12 @@ struct Batch {
     uint32_t* d_crc = nullptr;
     uint8_t* d_bwt = nullptr;
     uint32_t* d_orig = nullptr;
-    // BWT (bwt.hip): per-block SA, bucket queue, large-bucket lists, group lists
+    // BWT (bwt.hip): per-block SA, group lists, counters
     uint32_t* d_sa = nullptr;
-    uint64_t* d_bq = nullptr;
-    uint32_t* d_bcnt = nullptr;  // [0] queued buckets, [1] blocks with large buckets, [2] blocks with
-                                 // groups, [3] [4] pull counters of the large / doubling kernels
-    bz2mi::BwtSeg* d_large = nullptr;
-    uint32_t* d_nlarge = nullptr;
+    uint32_t* d_bcnt = nullptr;  // [0, 64) small-queue shard counts, [64 + 64 d) level-d queue shard counts,
+                                 // [768] blocks with groups, [769] doubling pull
+                                 // counter, [8 + d] level-d queue entries
     uint32_t* d_ngroups = nullptr;
-    uint32_t* d_clist = nullptr;
     uint32_t* d_p2list = nullptr;
     bz2mi::BwtSeg* d_groups = nullptr;
     // MTF / Huffman
@@ -82,8 +79,7 @@ struct Batch {
     hipEvent_t evA = nullptr, evM = nullptr, evFree = nullptr;
 
     std::vector<void*> ptrs() const {
-        return {d_blocks, d_lens, d_crc, d_bwt, d_orig, d_sa, d_bq, d_bcnt, d_large, d_nlarge, d_ngroups, d_clist,
-                d_p2list, d_groups, d_mtf, d_mtflen, d_alpha, d_hist, d_present, d_seed, d_payload,
+        return {d_blocks, d_lens, d_crc, d_bwt, d_orig, d_sa, d_bcnt, d_ngroups, d_p2list, d_groups, d_mtf, d_mtflen, d_alpha, d_hist, d_present, d_seed, d_payload,
                 d_pbits, d_offs};
     }
 };
@@ -107,6 +103,12 @@ struct bz2mi_ctx {
     uint32_t* d_out = nullptr;   // staging for the host-driven assembly
     size_t out_words = 0;
     uint8_t* d_scratch = nullptr;  // BWT workgroup slots (one BWT runs at a time: stream sA)
+    uint64_t* d_sq = nullptr;      // BWT small-segment queue (all blocks of a batch)
+    bz2mi::BwtItem* d_lq[2] = {nullptr, nullptr};  // BWT level queues (ping-pong)
+    uint64_t* d_tq[2] = {nullptr, nullptr};         // BWT per-block tie-group lists (ping-pong)
+    uint32_t* d_tc = nullptr;                       // their per-block counts (2 x blocks)
+    int small_grid = 0;                             // resident workgroups of bwt_small_kernel
+    int bwtq_blocks = 0;           // capacity of the queues in blocks
     uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
     uint32_t* d_crctab = nullptr;
     bz2mi::StreamDev* d_sd = nullptr;
@@ -175,12 +177,8 @@ int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks) {
     if ((r = dalloc(&t.d_bwt, B * c->stride))) return r;
     if ((r = dalloc(&t.d_orig, B))) return r;
     if ((r = dalloc(&t.d_sa, B * c->stride))) return r;
-    if ((r = dalloc(&t.d_bq, B * 256))) return r;
-    if ((r = dalloc(&t.d_bcnt, 8))) return r;
-    if ((r = dalloc(&t.d_large, B * 256))) return r;
-    if ((r = dalloc(&t.d_nlarge, B))) return r;
+    if ((r = dalloc(&t.d_bcnt, 1024))) return r;
     if ((r = dalloc(&t.d_ngroups, B))) return r;
-    if ((r = dalloc(&t.d_clist, B))) return r;
     if ((r = dalloc(&t.d_p2list, B))) return r;
     if ((r = dalloc(&t.d_groups, B * bz2mi::bwt_group_stride(c->stride)))) return r;
     if ((r = dalloc(&t.d_mtf, B * c->mtf_stride))) return r;
@@ -228,25 +226,66 @@ int stage_front(bz2mi_ctx* c, Batch& t, const uint8_t* d_x, size_t n, uint64_t f
 
 int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     using namespace bz2mi;
-    HIPCHECK(hipMemsetAsync(t.d_bcnt, 0, 8 * sizeof(uint32_t), s));
+    if (nb > c->bwtq_blocks) {  // queues are shared by the batches: BWTs run one at a time
+        HIPCHECK(hipStreamSynchronize(s));
+        for (void* p : {(void*)c->d_sq, (void*)c->d_lq[0], (void*)c->d_lq[1], (void*)c->d_tq[0], (void*)c->d_tq[1],
+                        (void*)c->d_tc})
+            if (p) (void)hipFree(p);
+        c->d_sq = nullptr;
+        c->d_lq[0] = c->d_lq[1] = nullptr;
+        c->d_tq[0] = c->d_tq[1] = nullptr;
+        c->d_tc = nullptr;
+        c->bwtq_blocks = 0;
+        const size_t B = (size_t)std::max(nb, 16);
+        const size_t Bs = (B + kBwtShards - 1) / kBwtShards;  // blocks per shard
+        int r;
+        if ((r = dalloc(&c->d_sq, kBwtShards * Bs * bwt_squeue_per_block(c->S)))) return r;
+        if ((r = dalloc(&c->d_lq[0], kBwtShards * Bs * bwt_lqueue_per_block(c->S)))) return r;
+        if ((r = dalloc(&c->d_lq[1], kBwtShards * Bs * bwt_lqueue_per_block(c->S)))) return r;
+        if ((r = dalloc(&c->d_tq[0], B * bwt_squeue_per_block(c->S)))) return r;
+        if ((r = dalloc(&c->d_tq[1], B * bwt_squeue_per_block(c->S)))) return r;
+        if ((r = dalloc(&c->d_tc, 2 * B))) return r;
+        c->bwtq_blocks = (int)B;
+    }
+    const size_t Bs = ((size_t)c->bwtq_blocks + kBwtShards - 1) / kBwtShards;
+    const size_t scap = Bs * bwt_squeue_per_block(c->S), lcap = Bs * bwt_lqueue_per_block(c->S);
+    const size_t tcap = bwt_squeue_per_block(c->S);
+    HIPCHECK(hipMemsetAsync(t.d_bcnt, 0, 1024 * sizeof(uint32_t), s));
+    HIPCHECK(hipMemsetAsync(t.d_ngroups, 0, nb * sizeof(uint32_t), s));
+    HIPCHECK(hipMemsetAsync(c->d_tc, 0, nb * sizeof(uint32_t), s));
     const int slots = std::min(nb, c->bwt_slots);
+    uint32_t* scount = t.d_bcnt;             // kBwtShards counters
+    uint32_t* lcount = t.d_bcnt + kBwtShards;  // level d: lcount + d * kBwtShards (queue d_lq[d & 1])
+    uint32_t* tc[2] = {c->d_tc, c->d_tc + c->bwtq_blocks};
+    uint32_t* p2count = t.d_bcnt + 768;
+    uint32_t* pull = t.d_bcnt + 769;
     hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
-                       t.d_bwt, t.d_orig, t.d_bq, t.d_bcnt, t.d_large, t.d_nlarge, t.d_ngroups, t.d_clist,
-                       t.d_bcnt + 1, t.d_present);
+                       t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap, t.d_present);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");
-    hipLaunchKernelGGL(bwt_small_kernel, dim3(c->cus * 8), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, t.d_sa,
-                       t.d_bwt, t.d_orig, t.d_bq, t.d_bcnt, t.d_groups, t.d_ngroups, t.d_p2list, t.d_bcnt + 2);
+    for (int d = 1; d <= kBwtLevels; ++d) {
+        hipLaunchKernelGGL(bwt_level_kernel, dim3(c->bwt_slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
+                           t.d_sa, t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, c->d_lq[d & 1],
+                           lcount + d * kBwtShards, c->d_lq[(d + 1) & 1], lcount + (d + 1) * kBwtShards, lcap,
+                           c->d_sq, scount, scap, t.d_groups, t.d_ngroups, t.d_p2list, p2count,
+                           d == kBwtLevels ? 1 : 0);
+        HIPCHECK(hipGetLastError());
+    }
+    STAGE_DONE("bwt_levels");
+    hipLaunchKernelGGL(bwt_small_kernel, dim3(c->small_grid), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
+                       t.d_sa, t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_tq[0], tc[0], tcap);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_small");
-    hipLaunchKernelGGL(bwt_large_kernel, dim3(slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
-                       t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, t.d_large, t.d_nlarge,
-                       t.d_groups, t.d_ngroups, t.d_p2list, t.d_bcnt + 2, t.d_clist, t.d_bcnt + 1, t.d_bcnt + 3);
-    HIPCHECK(hipGetLastError());
-    STAGE_DONE("bwt_large");
+    for (int r = 0; r < kBwtTieRounds; ++r) {
+        hipLaunchKernelGGL(bwt_tie_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, t.d_sa,
+                           t.d_bwt, t.d_orig, c->d_tq[r & 1], tc[r & 1], c->d_tq[(r + 1) & 1], tc[(r + 1) & 1], tcap,
+                           t.d_groups, t.d_ngroups, t.d_p2list, p2count, r + 1 == kBwtTieRounds ? 1 : 0);
+        HIPCHECK(hipGetLastError());
+    }
+    STAGE_DONE("bwt_ties");
     hipLaunchKernelGGL(bwt_double_kernel, dim3(slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
                        t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, t.d_groups, t.d_ngroups,
-                       t.d_p2list, t.d_bcnt + 2, t.d_bcnt + 4);
+                       t.d_p2list, p2count, pull);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt");
     return BZ2MI_OK;
@@ -616,6 +655,13 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
     c->cus = cus;
     c->bwt_slots = cus * 4;
+    {
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(bz2mi::bwt_small_kernel),
+                                                         256, 0) != hipSuccess || occ < 1)
+            occ = 2;
+        c->small_grid = cus * occ;
+    }
     if (dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S)) ||
         dalloc(&c->d_state, (size_t)c->p * bz2mi::kMaxAlpha) || dalloc(&c->d_sd, 1) || dalloc(&c->d_vol, 4)) {
         bz2mi_destroy(c);
@@ -643,7 +689,8 @@ void bz2mi_destroy(bz2mi_ctx* c) {
     (void)hipSetDevice(c->device);
     for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB})
         if (st) (void)hipStreamSynchronize(st);
-    std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
+    std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_sq, c->d_lq[0], c->d_lq[1], c->d_tq[0], c->d_tq[1],
+                               c->d_tc, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
                                c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd,
                                c->d_starts, c->d_nb};
     for (const Batch& t : c->sets) {

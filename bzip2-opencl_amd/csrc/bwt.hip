@@ -57,6 +57,8 @@ struct BwtShared {
     uint64_t tmp64b[NW];
     uint32_t cnt[8];     // list counters
     uint32_t bcast[4];
+    uint32_t bat_start[256];  // batches of small children (pack_children)
+    uint32_t bat_len[256];    // length | one-child flag << 31
 };
 
 using Seg = BwtSeg;
@@ -184,6 +186,11 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&key)[E], uint32_t (&lo)[
     bitonic_from<E, WITH_LO, 2>(key, lo);
 }
 
+// Small-queue entries: block | start | len-1 | depth (22 | 20 | 9 | 13 bits).
+__host__ __device__ inline uint64_t sq_pack(uint32_t b, uint32_t start, uint32_t len, uint32_t depth) {
+    return ((uint64_t)b << 42) | ((uint64_t)start << 22) | ((uint64_t)(len - 1) << 13) | depth;
+}
+
 // Where a sort puts the groups (equal keys, size > 1) it leaves behind: a list
 // with a capacity; the first group of a block can also enlist the block for
 // the phase-2 kernel.
@@ -194,16 +201,34 @@ struct GroupSink {
     uint32_t* worklist;  // nullptr inside the per-block kernel
     uint32_t* wcount;
     uint32_t block;
+    uint64_t* tq;        // non-null: tie groups go to this global queue (with their depth)
+    uint32_t* tcount;
 
     __device__ __forceinline__ void push(Seg g) const {
         const uint32_t slot = atomicAdd(counter, 1u);
         if (slot < cap) out[slot] = g;
         if (worklist && slot == 0) worklist[atomicAdd(wcount, 1u)] = block;
     }
+    // Called by every active lane; the lanes with `want` push `g` whose
+    // rotations share `depth` bytes.  Tie-queue pushes take one atomic per
+    // wave (the queue counter is shared by the whole chip).
+    __device__ __forceinline__ void push_agg(bool want, Seg g, uint32_t depth) const {
+        if (!tq) {
+            if (want) push(g);
+            return;
+        }
+        const uint64_t m = __ballot(want);
+        if (m == 0) return;
+        const int leader = __builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(tcount, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (want) tq[base + (uint32_t)__popcll(m & __lanemask_lt())] = sq_pack(block, g.start, g.len, depth);
+    }
 };
 
 __device__ __forceinline__ GroupSink local_sink(Seg* out, uint32_t* counter) {
-    return GroupSink{out, counter, 0xffffffffu, nullptr, nullptr, 0};
+    return GroupSink{out, counter, 0xffffffffu, nullptr, nullptr, 0, nullptr, nullptr};
 }
 
 __device__ __forceinline__ uint8_t bwt_byte(const uint8_t* __restrict__ T, int n, uint32_t i) {
@@ -217,6 +242,11 @@ __device__ __forceinline__ uint8_t bwt_byte(const uint8_t* __restrict__ T, int n
 //   positions get their BWT byte (and origPtr) directly; labels are deferred.
 // mode 1 (phase 2): keys = (snapshot label << 20) | index from ka[]; members
 //   get their new labels.
+template <int E, int MODE>
+__device__ __forceinline__ void wave_sort_emit(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
+                               uint64_t (&key)[E], uint32_t (&lo)[E], const GroupSink& sink,
+                               uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig);
+
 template <int E, int MODE>
 __device__ void wave_sort_segment(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
                                   const GroupSink& sink, uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig) {
@@ -243,6 +273,30 @@ __device__ void wave_sort_segment(const uint8_t* __restrict__ T, int n, Scratch&
             lo[e] = ~0u;
         }
     }
+    wave_sort_emit<E, MODE>(T, n, s, seg, d, key, lo, sink, bwt, orig);
+}
+
+// Sort keys already loaded (blocked or any layout; padding = ~0) and emit:
+// item g of the sorted order lands at seg.start + g.
+template <int E, int MODE>
+__device__ __forceinline__ void wave_sort_emit(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
+                               uint64_t (&key)[E], uint32_t (&lo)[E], const GroupSink& sink,
+                               uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig) {
+    const int lane = lane_id();
+    uint32_t d0 = 8;  // bytes the keys compare
+    if constexpr (MODE == 0) {
+        // a valid key of eight 0xff bytes would tie with the padding: then
+        // this segment sorts on 7 bytes first (the deepening goes on from there)
+        bool ff = false;
+#pragma unroll
+        for (int e = 0; e < E; ++e) ff |= lo[e] != ~0u && key[e] == ~0ull;
+        if (__ballot(ff)) {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if (lo[e] != ~0u) key[e] >>= 8;
+            d0 = 7;
+        }
+    }
     wave_bitonic<E, MODE == 0>(key, lo);
     constexpr int kShift = MODE == 0 ? 0 : kIdxBits;
     // group flags (key part only), group starts by a max-scan, group ends by
@@ -266,18 +320,21 @@ __device__ void wave_sort_segment(const uint8_t* __restrict__ T, int n, Scratch&
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t g = (uint32_t)(lane * E + e);
-        if (g >= seg.len) continue;
+        const bool valid = g < seg.len;
         const uint32_t i = MODE == 0 ? lo[e] & 0xffffffu : (uint32_t)(key[e] & ((1u << kIdxBits) - 1u));
         const uint32_t gs = gsl[e] > before ? gsl[e] : before;
-        s.sa[seg.start + g] = i;
-        if (MODE == 0) {
-            bwt[seg.start + g] = (uint8_t)(lo[e] >> 24);
-            if (i == 0) *orig = seg.start + g;
-        } else {
-            s.rank[i] = seg.start + gs;
+        if (valid) {
+            s.sa[seg.start + g] = i;
+            if (MODE == 0) {
+                bwt[seg.start + g] = (uint8_t)(lo[e] >> 24);
+                if (i == 0) *orig = seg.start + g;
+            } else {
+                s.rank[i] = seg.start + gs;
+            }
         }
         const bool nf = e + 1 < E ? flag[e + 1 < E ? e + 1 : 0] : next_lane_flag;
-        if ((g + 1 == seg.len || nf) && g > gs) sink.push(Seg{seg.start + gs, g - gs + 1});
+        // every lane calls (the tie-queue push is wave-aggregated)
+        sink.push_agg(valid && (g + 1 == seg.len || nf) && g > gs, Seg{seg.start + gs, g - gs + 1}, d + d0);
     }
 }
 
@@ -431,52 +488,6 @@ __device__ void wg_sort_group(Scratch& s, Seg seg, BwtShared& sh, Seg* out, uint
     }
 }
 
-// Phase 1 large bucket at depth d: partition by byte d; children go to the
-// small list, the next large list, or are finished (size 1 / depth limit).
-__device__ void wg_partition(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d, BwtShared& sh,
-                             Seg* large_next, const GroupSink& sink, uint8_t* __restrict__ bwt,
-                             uint32_t* __restrict__ orig) {
-    seg.start = uniform(seg.start);
-    seg.len = uniform(seg.len);
-    const int t = threadIdx.x;
-    sh.hist[t] = 0;
-    __syncthreads();
-    for (uint32_t k = t; k < seg.len; k += NT) {
-        const uint32_t i = s.sa[seg.start + k];
-        s.vb[seg.start + k] = i;
-        atomicAdd(&sh.hist[byte_at(T, n, i + d)], 1u);
-    }
-    __syncthreads();
-    const uint32_t c = sh.hist[t];
-    uint32_t total;
-    const uint32_t ex = wg_excl_sum<NT>(c, sh.tmp, &total);
-    sh.base[t] = ex;
-    __syncthreads();
-    // stable placement is not needed: later sorts break ties by index
-    for (uint32_t k = t; k < seg.len; k += NT) {
-        const uint32_t i = s.vb[seg.start + k];
-        const uint32_t slot = atomicAdd(&sh.base[byte_at(T, n, i + d)], 1u);
-        s.sa[seg.start + slot] = i;
-    }
-    __syncthreads();
-    // children: bucket t spans [ex, ex + c)
-    if (c == 1) {
-        const uint32_t i = s.sa[seg.start + ex];
-        bwt[seg.start + ex] = bwt_byte(T, n, i);
-        if (i == 0) *orig = seg.start + ex;
-    } else if (c > 1) {
-        const Seg ch{seg.start + ex, c};
-        if (c <= (uint32_t)kSmall) {
-            s.small[atomicAdd(&sh.cnt[0], 1u)] = ch;
-        } else if (d + 1 >= (uint32_t)kMaxDepth) {
-            sink.push(ch);
-        } else {
-            large_next[atomicAdd(&sh.cnt[3], 1u)] = ch;
-        }
-    }
-    __syncthreads();
-}
-
 // ---- phase 1a: counting sort of the rotations by their first byte into sa.
 // Thread t gets bucket t: start *ex, size *c.
 __device__ void count_sort_first(const uint8_t* __restrict__ T, int n, uint32_t* __restrict__ sa, BwtShared& sh,
@@ -511,49 +522,6 @@ __device__ void count_sort_first(const uint8_t* __restrict__ T, int n, uint32_t*
     __syncthreads();
     *c_out = c;
     *ex_out = ex;
-}
-
-// ---- phase 1b: expects the small / large bucket lists (sh.cnt[0], [1])
-// (expects the large list in s.large, count sh.cnt[1], no small buckets yet;
-// groups go to `sink`)
-__device__ void bwt_levels(const uint8_t* __restrict__ T, int n, uint8_t* __restrict__ out,
-                           uint32_t* __restrict__ orig, Scratch& s, BwtShared& sh, const GroupSink& sink,
-                           bool stamp) {
-    const int t = threadIdx.x;
-    // ---- phase 1b: levels of (small sorts, large partitions)
-    uint32_t depth = 1;
-    Seg* large = s.large;
-    Seg* large_next = s.large2;
-    for (;;) {
-        // small buckets: one wave each, keys = the 8 bytes at `depth`
-        const uint32_t nsmall = uniform(sh.cnt[0]);
-        if (t == 0) sh.cnt[4] = 0;
-        __syncthreads();
-        for (;;) {
-            uint32_t idx = 0;
-            if (lane_id() == 0) idx = atomicAdd(&sh.cnt[4], 1u);
-            idx = uniform(__shfl(idx, 0));
-            if (idx >= nsmall) break;
-            wave_sort_any<0>(T, n, s, s.small[idx], depth, sink, out, orig);
-        }
-        __syncthreads();
-        BZ2MI_PHASE(g_bwt_phase, 2, stamp && depth == 1);
-        const uint32_t nlarge = uniform(sh.cnt[1]);
-        if (nlarge == 0) break;
-        if (t == 0) {
-            sh.cnt[0] = 0;
-            sh.cnt[3] = 0;
-        }
-        __syncthreads();
-        for (uint32_t q = 0; q < nlarge; ++q) wg_partition(T, n, s, large[q], depth, sh, large_next, sink, out, orig);
-        if (t == 0) sh.cnt[1] = sh.cnt[3];
-        __syncthreads();
-        Seg* tmpl = large;
-        large = large_next;
-        large_next = tmpl;
-        depth++;
-    }
-    BZ2MI_PHASE(g_bwt_phase, 3, stamp);
 }
 
 // ---- labels, phase 2 and the reordered BWT bytes: expects the groups left
@@ -654,122 +622,380 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
     BZ2MI_PHASE(g_bwt_phase, 5, stamp);
 }
 
-// ---- a first-byte bucket (<= 512 rotations) on one wave: counting sort by
-// the second byte into sub-buckets, then every rotation of a sub-bucket of
-// <= kSub finds its place by counting the smaller (next 8 bytes, index) pairs
-// of its sub-bucket; larger sub-buckets get the wave bitonic sort at depth 2.
-// For data with a wide alphabet the sub-buckets hold one or two rotations,
-// so this is a few operations per rotation instead of a 512-wide network.
+// ---- a bucket of <= 512 rotations with a common prefix of d bytes, on one
+// wave.  The 8-byte keys at depth d are loaded once and counting-sorted by
+// their first byte (byte d) into LDS sub-buckets.  Then either
+//   * text-like segments (most rotations in sub-buckets of > kSub): one wave
+//     sort of the whole segment on the keys, or
+//   * every rotation of a sub-bucket of <= kSub finds its place by counting
+//     the smaller (key, index) pairs of its sub-bucket (wide alphabets: one
+//     or two rotations per sub-bucket), and larger sub-buckets get a wave
+//     sort of their own;
+// all from LDS.  Tie groups go to the sink with their depth.
 constexpr int kSub = 32;
 
 struct Bucket2Lds {
     uint32_t base[257];
-    uint64_t key[kSmall];
+    uint64_t key[kSmall];  // 8 bytes at depth d, grouped by byte d
     uint32_t idx[kSmall];  // rotation index | BWT byte << 24
 };
 
-__device__ void wave_sort_bucket2(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, const GroupSink& sink,
-                                  uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig, Bucket2Lds& L) {
+// wave sort of LDS items [b0, b0+m) (m <= 64*E), emitted at seg.start + b0
+template <int E>
+__device__ __forceinline__ void wave_sort_lds(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t start,
+                                              uint32_t b0, uint32_t m, uint32_t d, const GroupSink& sink,
+                                              uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
+                                              const Bucket2Lds& L) {
+    const int lane = lane_id();
+    uint64_t key[E];
+    uint32_t lo[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(lane * E + e);
+        key[e] = g < m ? L.key[b0 + g] : ~0ull;
+        lo[e] = g < m ? L.idx[b0 + g] : ~0u;
+    }
+    wave_sort_emit<E, 0>(T, n, s, Seg{start + b0, m}, d, key, lo, sink, bwt, orig);
+}
+
+__device__ __forceinline__ void wave_sort_lds_any(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t start,
+                                               uint32_t b0, uint32_t m, uint32_t d, const GroupSink& sink,
+                                               uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
+                                               const Bucket2Lds& L) {
+    if (m <= 64) wave_sort_lds<1>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+    else if (m <= 128) wave_sort_lds<2>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+    else if (m <= 256) wave_sort_lds<4>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+    else wave_sort_lds<8>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+}
+
+__device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
+                                  const GroupSink& sink, uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
+                                  Bucket2Lds& L) {
     constexpr int E = kSmall / 64;
     const int lane = lane_id();
 #pragma unroll
     for (int j = 0; j < 4; ++j) L.base[lane * 4 + j] = 0;
-    uint32_t ii[E], c2[E], slot[E];
-    uint64_t key[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t g = (uint32_t)(e * 64 + lane);
-        c2[e] = 0;
-        slot[e] = 0;
-        ii[e] = 0;
-        key[e] = 0;
-        if (g < seg.len) {
-            const uint32_t i = s.sa[seg.start + g];
-            uint32_t p1 = i + 1, p2 = i + 2;
-            if (p1 >= (uint32_t)n) p1 -= (uint32_t)n;
-            if (p2 >= (uint32_t)n) p2 %= (uint32_t)n;
-            c2[e] = T[p1];
-            key[e] = load8(T, n, p2);
-            ii[e] = i | ((uint32_t)bwt_byte(T, n, i) << 24);
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-        if ((uint32_t)(e * 64 + lane) < seg.len) slot[e] = atomicAdd(&L.base[c2[e]], 1u);
-    // counts -> sub-bucket starts (lane l: counters 4l..4l+3)
     {
-        const uint32_t h0 = L.base[lane * 4], h1 = L.base[lane * 4 + 1], h2 = L.base[lane * 4 + 2],
-                       h3 = L.base[lane * 4 + 3];
-        const uint32_t sum = h0 + h1 + h2 + h3;
-        const uint32_t ex = wave_incl_sum(sum) - sum;
-        L.base[lane * 4] = ex;
-        L.base[lane * 4 + 1] = ex + h0;
-        L.base[lane * 4 + 2] = ex + h0 + h1;
-        L.base[lane * 4 + 3] = ex + h0 + h1 + h2;
-        if (lane == 0) L.base[256] = seg.len;
-    }
-    uint32_t pos[E];
+        uint32_t ii[E], slot[E];
+        uint64_t key[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        pos[e] = 0;
-        if ((uint32_t)(e * 64 + lane) < seg.len) {
-            pos[e] = L.base[c2[e]] + slot[e];
-            L.key[pos[e]] = key[e];
-            L.idx[pos[e]] = ii[e];
+        for (int e = 0; e < E; ++e) {
+            const uint32_t g = (uint32_t)(e * 64 + lane);
+            slot[e] = 0;
+            ii[e] = 0;
+            key[e] = 0;
+            if (g < seg.len) {
+                const uint32_t i = s.sa[seg.start + g];
+                uint32_t p = i + d;
+                if (p >= (uint32_t)n) p %= (uint32_t)n;
+                key[e] = load8(T, n, p);
+                ii[e] = i | ((uint32_t)bwt_byte(T, n, i) << 24);
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if ((uint32_t)(e * 64 + lane) < seg.len) slot[e] = atomicAdd(&L.base[key[e] >> 56], 1u);
+        // counts -> sub-bucket starts (lane l: counters 4l..4l+3)
+        {
+            const uint32_t h0 = L.base[lane * 4], h1 = L.base[lane * 4 + 1], h2 = L.base[lane * 4 + 2],
+                           h3 = L.base[lane * 4 + 3];
+            const uint32_t sum = h0 + h1 + h2 + h3;
+            const uint32_t ex = wave_incl_sum(sum) - sum;
+            L.base[lane * 4] = ex;
+            L.base[lane * 4 + 1] = ex + h0;
+            L.base[lane * 4 + 2] = ex + h0 + h1;
+            L.base[lane * 4 + 3] = ex + h0 + h1 + h2;
+            if (lane == 0) L.base[256] = seg.len;
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if ((uint32_t)(e * 64 + lane) < seg.len) {
+                const uint32_t pos = L.base[key[e] >> 56] + slot[e];
+                L.key[pos] = key[e];
+                L.idx[pos] = ii[e];
+            }
         }
     }
-    bool any_big = false;
+    // rotations in sub-buckets of > kSub (lane l: sub-buckets 4l..4l+3)
+    uint32_t inbig = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t c = (uint32_t)(lane * 4 + j);
+        const uint32_t m = L.base[c + 1] - L.base[c];
+        inbig += m > (uint32_t)kSub ? m : 0u;
+    }
+    const uint32_t nbig = wave_sum(inbig);
+    if (2 * nbig > seg.len) {
+        wave_sort_lds_any(T, n, s, seg.start, 0, seg.len, d, sink, bwt, orig, L);
+        return;
+    }
+    // small sub-buckets: ranks by counting (striped positions p = e*64 + lane)
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        if ((uint32_t)(e * 64 + lane) >= seg.len) continue;
-        const uint32_t b0 = L.base[c2[e]], m = L.base[c2[e] + 1] - b0;
-        const uint32_t i = ii[e] & 0xffffffu;
-        if (m > (uint32_t)kSub) {  // sorted below as a whole
-            s.sa[seg.start + pos[e]] = i;
-            any_big = true;
-            continue;
-        }
+        const uint32_t p = (uint32_t)(e * 64 + lane);
+        const bool inseg = p < seg.len;
+        const uint64_t k = inseg ? L.key[p] : 0ull;
+        const uint32_t ii = inseg ? L.idx[p] : 0u;
+        const uint32_t c = (uint32_t)(k >> 56);
+        const uint32_t b0 = L.base[c], m = inseg ? L.base[c + 1] - b0 : 0u;
+        const bool mine = inseg && m <= (uint32_t)kSub;
+        const uint32_t i = ii & 0xffffffu;
         uint32_t lt = 0, le = 0, eqlt = 0;
-        for (uint32_t q = 0; q < m; ++q) {
+        for (uint32_t q = 0; q < (mine ? m : 0u); ++q) {
             const uint64_t kq = L.key[b0 + q];
             const uint32_t iq = L.idx[b0 + q] & 0xffffffu;
-            lt += kq < key[e];
-            le += kq <= key[e];
-            eqlt += (kq == key[e]) & (iq < i);
+            lt += kq < k;
+            le += kq <= k;
+            eqlt += (kq == k) & (iq < i);
         }
         const uint32_t fin = seg.start + b0 + lt + eqlt;
-        s.sa[fin] = i;
-        bwt[fin] = (uint8_t)(ii[e] >> 24);
-        if (i == 0) *orig = fin;
-        if (le - lt >= 2 && eqlt == 0) sink.push(Seg{seg.start + b0 + lt, le - lt});
+        if (mine) {
+            s.sa[fin] = i;
+            bwt[fin] = (uint8_t)(ii >> 24);
+            if (i == 0) *orig = fin;
+        }
+        sink.push_agg(mine && le - lt >= 2 && eqlt == 0, Seg{seg.start + b0 + lt, le - lt}, d + 8);
     }
-    // sub-buckets too large for counting: wave bitonic at depth 2
-    uint64_t bigmask = __ballot(any_big);
-    if (bigmask) {
-        __threadfence_block();  // the SA entries just written are read by other lanes
-        for (int c = 0; c < 256; ++c) {
+    if (nbig) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t c = (uint32_t)(lane * 4 + j);
             const uint32_t b0 = L.base[c], m = L.base[c + 1] - b0;
-            if (m > (uint32_t)kSub) wave_sort_any<0>(T, n, s, Seg{seg.start + b0, m}, 2, sink, bwt, orig);
+            uint64_t big = __ballot(m > (uint32_t)kSub);
+            while (big) {
+                const int l = __builtin_ctzll(big);
+                big &= big - 1;
+                wave_sort_lds_any(T, n, s, seg.start, (uint32_t)__shfl((int)b0, l), (uint32_t)__shfl((int)m, l), d,
+                                  sink, bwt, orig, L);
+            }
         }
     }
 }
 
-constexpr int kQLenBits = 10, kQStartBits = 20;
+// ---- a tie group (<= kTieThread rotations with a common prefix of d
+// bytes) on one thread: keys = the next 8 bytes, ranks by counting, ties
+// with the rotation index; subgroups go to the sink at depth d+8.
+constexpr int kTieThread = 16;
 
+struct TieLds {
+    uint64_t key[kTieThread][NT];
+    uint32_t idx[kTieThread][NT];
+};
+
+__device__ void thread_sort_ties(const uint8_t* __restrict__ T, int n, uint32_t* __restrict__ sa, Seg seg,
+                                 uint32_t d, const GroupSink& sink, uint8_t* __restrict__ bwt,
+                                 uint32_t* __restrict__ orig, TieLds& L) {
+    const int t = threadIdx.x;
+    for (uint32_t k = 0; k < seg.len; ++k) {
+        const uint32_t i = sa[seg.start + k];
+        uint32_t p = i + d;
+        if (p >= (uint32_t)n) p %= (uint32_t)n;
+        L.key[k][t] = load8(T, n, p);
+        L.idx[k][t] = i;
+    }
+    for (uint32_t a = 0; a < seg.len; ++a) {
+        const uint64_t ka = L.key[a][t];
+        const uint32_t ia = L.idx[a][t];
+        uint32_t lt = 0, le = 0, eqlt = 0;
+        for (uint32_t q = 0; q < seg.len; ++q) {
+            const uint64_t kq = L.key[q][t];
+            lt += kq < ka;
+            le += kq <= ka;
+            eqlt += (kq == ka) & (L.idx[q][t] < ia);
+        }
+        const uint32_t fin = seg.start + lt + eqlt;
+        sa[fin] = ia;
+        bwt[fin] = bwt_byte(T, n, ia);
+        if (ia == 0) *orig = fin;
+        sink.push_agg(le - lt >= 2 && eqlt == 0, Seg{seg.start + lt, le - lt}, d + 8);
+    }
+}
+
+// ---- sharded queues: 64 shards (shard = block & 63), each with its own
+// counter and capacity, so that the producers of the whole chip do not all
+// hit one atomic counter.  Consumers index the concatenation of the shards.
+constexpr int kShards = 64;
+
+template <typename Item>
+struct Sharded {
+    Item* base;
+    uint32_t* counts;  // kShards counters
+    size_t cap;        // entries per shard
+    __device__ __forceinline__ uint32_t reserve(uint32_t b, uint32_t k) const {
+        return atomicAdd(&counts[b & (kShards - 1)], k);
+    }
+    __device__ __forceinline__ void put(uint32_t b, uint32_t slot, const Item& it) const {
+        base[(size_t)(b & (kShards - 1)) * cap + slot] = it;
+    }
+};
+
+struct ShardIndex {
+    uint32_t pre[kShards + 1];
+};
+
+// all threads call; wave 0 builds the prefix table; returns the total
+__device__ __forceinline__ uint32_t shard_index_load(const uint32_t* __restrict__ counts, ShardIndex& si) {
+    if (threadIdx.x < 64) {
+        const uint32_t c = counts[threadIdx.x];
+        const uint32_t inc = wave_incl_sum(c);
+        si.pre[threadIdx.x + 1] = inc;
+        if (threadIdx.x == 0) si.pre[0] = 0;
+    }
+    __syncthreads();
+    return uniform(si.pre[kShards]);
+}
+
+// entry offset of the q-th item of the concatenation (q < total)
+__device__ __forceinline__ size_t shard_locate(const ShardIndex& si, uint32_t q, size_t cap) {
+    uint32_t lo = 0, hi = kShards;  // pre[lo] <= q < pre[hi]
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (si.pre[mid] <= q) lo = mid;
+        else hi = mid;
+    }
+    return (size_t)lo * cap + (q - si.pre[lo]);
+}
+
+// Pack the children of a partition (counts in sh.hist, in byte order from
+// relative position 0) into batches for the small kernel: runs of
+// consecutive children of <= kSmall rotations, at most kSmall rotations per
+// batch, large children break runs.  A batch of one child is sorted from
+// depth d+1, a batch of several from depth d (byte d separates them).
+// Batches with no child of >= 2 rotations are dropped (singletons are final).
+// Thread 0 packs; returns the batch count (sh.bat_*).
+__device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
+    if (threadIdx.x == 0) {
+        uint32_t nb = 0, pos = 0, bs = 0, bl = 0, nch = 0;
+        bool useful = false;
+        for (int c = 0; c < 256; ++c) {
+            const uint32_t m = sh.hist[c];
+            if (m == 0) continue;
+            const bool big = m > (uint32_t)kSmall;
+            if (bl && (big || bl + m > (uint32_t)kSmall)) {
+                if (useful) {
+                    sh.bat_start[nb] = bs;
+                    sh.bat_len[nb] = bl | (nch == 1 ? 0x80000000u : 0u);
+                    nb++;
+                }
+                bl = 0;
+                nch = 0;
+                useful = false;
+            }
+            if (!big) {
+                if (bl == 0) bs = pos;
+                bl += m;
+                nch++;
+                useful |= m > 1;
+            }
+            pos += m;
+        }
+        if (bl && useful) {
+            sh.bat_start[nb] = bs;
+            sh.bat_len[nb] = bl | (nch == 1 ? 0x80000000u : 0u);
+            nb++;
+        }
+        sh.cnt[7] = nb;
+    }
+    __syncthreads();
+    return uniform(sh.cnt[7]);
+}
+
+// Partition the large segment `seg` (common prefix of d bytes) of block b by
+// byte d with the whole workgroup; children: size 1 is final, runs of small
+// ones go to the small queue as batches, larger ones to `large_out` or, at
+// the depth limit, to the group sink.  The segment is staged in LDS
+// (`stage`, kStage entries) or, when longer, in the global `spill` area.
+constexpr int kStage = 6144;
+
+struct LevelLds {
+    BwtShared sh;
+    ShardIndex si;
+    uint32_t stage[kStage];
+};
+
+template <typename LargeOut>
+__device__ void partition_segment(const uint8_t* __restrict__ T, int n, uint32_t b, uint32_t* __restrict__ sa,
+                                  Seg seg, uint32_t d, LevelLds& L, uint32_t* __restrict__ spill,
+                                  const Sharded<uint64_t>& sq, const LargeOut& large_out, const GroupSink& sink,
+                                  uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig) {
+    BwtShared& sh = L.sh;
+    seg.start = uniform(seg.start);
+    seg.len = uniform(seg.len);
+    const int t = threadIdx.x;
+    uint32_t* cp = seg.len <= (uint32_t)kStage ? L.stage : spill;
+    sh.hist[t] = 0;
+    __syncthreads();
+    for (uint32_t k = t; k < seg.len; k += NT) {
+        const uint32_t i = sa[seg.start + k];
+        cp[k] = i;
+        atomicAdd(&sh.hist[byte_at(T, n, i + d)], 1u);
+    }
+    __syncthreads();
+    const uint32_t c = sh.hist[t];
+    uint32_t total;
+    const uint32_t ex = wg_excl_sum<NT>(c, sh.tmp, &total);
+    sh.base[t] = ex;
+    __syncthreads();
+    // stable placement is not needed: later sorts break ties by index
+    for (uint32_t k = t; k < seg.len; k += NT) {
+        const uint32_t i = cp[k];
+        const uint32_t slot = atomicAdd(&sh.base[byte_at(T, n, i + d)], 1u);
+        sa[seg.start + slot] = i;
+    }
+    const uint32_t nbat = pack_children(sh);
+    // large children: one reservation per workgroup
+    const bool deep = c > (uint32_t)kSmall && d + 1 >= (uint32_t)kMaxDepth;
+    const bool large = c > (uint32_t)kSmall && !deep;
+    uint32_t nl;
+    const uint32_t rl = wg_excl_sum<NT>(large ? 1u : 0u, sh.tmp, &nl);
+    if (t == 0) {
+        sh.bcast[1] = nbat ? sq.reserve(b, nbat) : 0u;
+        sh.bcast[2] = nl ? large_out.reserve(b, nl) : 0u;
+    }
+    __syncthreads();  // also orders the SA scatter before the final reads
+    if (c == 1) {
+        const uint32_t i = sa[seg.start + ex];
+        bwt[seg.start + ex] = bwt_byte(T, n, i);
+        if (i == 0) *orig = seg.start + ex;
+    } else if (large) {
+        large_out.put(b, sh.bcast[2] + rl, BwtItem{b, seg.start + ex, c, d + 1});
+    } else if (deep) {
+        sink.push(Seg{seg.start + ex, c});
+    }
+    if ((uint32_t)t < nbat) {
+        const uint32_t bl = sh.bat_len[t];
+        const uint32_t one = bl >> 31;
+        sq.put(b, sh.bcast[1] + t, sq_pack(b, seg.start + sh.bat_start[t], bl & 0x7fffffffu, d + one));
+    }
+    __syncthreads();
+}
+
+// next-level queue (global, all blocks) or the workgroup's own list
+struct GlobalLarge {
+    Sharded<BwtItem> q;
+    __device__ uint32_t reserve(uint32_t b, uint32_t k) const { return q.reserve(b, k); }
+    __device__ void put(uint32_t b, uint32_t slot, BwtItem it) const { q.put(b, slot, it); }
+};
+struct LocalLarge {
+    Seg* q;
+    uint32_t* count;  // LDS
+    __device__ uint32_t reserve(uint32_t, uint32_t k) const { return atomicAdd(count, k); }
+    __device__ void put(uint32_t, uint32_t slot, BwtItem it) const { q[slot] = Seg{it.start, it.len}; }
+};
 
 }  // namespace
 
 // ---- kernel 1: per block, counting sort of the rotations by their first
-// byte.  Buckets of <= 512 go to the queue of kernel 2 (all blocks), larger
-// ones to the block's large list for kernel 3.
+// byte.  Runs of small buckets go to the small queue as batches (all
+// blocks), larger buckets to the level-1 queue of the partition kernel.
 __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restrict__ blocks, size_t stride,
                                                          const uint32_t* __restrict__ lens, int nblocks,
                                                          uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
-                                                         uint32_t* __restrict__ orig_out, uint64_t* __restrict__ queue,
-                                                         uint32_t* __restrict__ qcount, Seg* __restrict__ large_all,
-                                                         uint32_t* __restrict__ nlarge, uint32_t* __restrict__ ngroups,
-                                                         uint32_t* __restrict__ clist, uint32_t* __restrict__ ccount,
-                                                         uint32_t* __restrict__ present_out) {
+                                                         uint32_t* __restrict__ orig_out, uint64_t* __restrict__ squeue,
+                                                         uint32_t* __restrict__ scount, size_t scap,
+                                                         BwtItem* __restrict__ lq, uint32_t* __restrict__ lcount,
+                                                         size_t lcap, uint32_t* __restrict__ present_out) {
     __shared__ BwtShared sh;
     const int b = blockIdx.x;
     if (b >= nblocks) return;
@@ -777,12 +1003,10 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
     const int n = (int)uniform(lens[b]);
     const uint8_t* T = blocks + (size_t)b * stride;
     uint8_t* out = bwt_out + (size_t)b * stride;
-    if (t == 0) ngroups[b] = 0;
     if (n <= 1) {
         if (t == 0) {
             if (n == 1) out[0] = T[0];
             orig_out[b] = 0;
-            nlarge[b] = 0;
         }
         if (t < 8) present_out[(size_t)b * 8 + t] = (n == 1 && (T[0] >> 5) == t) ? 1u << (T[0] & 31) : 0u;
         return;
@@ -802,90 +1026,182 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
         out[ex] = bwt_byte(T, n, i);
         if (i == 0) orig_out[b] = ex;
     }
-    const bool small = c > 1 && c <= (uint32_t)kSmall, large = c > (uint32_t)kSmall;
-    uint32_t nq, nl;
-    const uint32_t r = wg_excl_sum<NT>(small ? 1u : 0u, sh.tmp, &nq);
+    const Sharded<uint64_t> sq{squeue, scount, scap};
+    const Sharded<BwtItem> lqs{lq, lcount, lcap};
+    const uint32_t nbat = pack_children(sh);
+    const bool large = c > (uint32_t)kSmall;
+    uint32_t nl;
     const uint32_t rl = wg_excl_sum<NT>(large ? 1u : 0u, sh.tmp, &nl);
     if (t == 0) {
-        sh.bcast[0] = nq ? atomicAdd(qcount, nq) : 0u;
-        nlarge[b] = nl;
-        if (nl) clist[atomicAdd(ccount, 1u)] = (uint32_t)b;
+        sh.bcast[0] = nbat ? sq.reserve((uint32_t)b, nbat) : 0u;
+        sh.bcast[1] = nl ? lqs.reserve((uint32_t)b, nl) : 0u;
     }
     __syncthreads();
-    if (small)
-        queue[sh.bcast[0] + r] = ((uint64_t)b << (kQStartBits + kQLenBits)) | ((uint64_t)ex << kQLenBits) | (c - 1);
-    if (large) large_all[(size_t)b * 256 + rl] = Seg{ex, c};
+    if ((uint32_t)t < nbat) {
+        const uint32_t bl = sh.bat_len[t];
+        sq.put((uint32_t)b, sh.bcast[0] + t, sq_pack((uint32_t)b, sh.bat_start[t], bl & 0x7fffffffu, bl >> 31));
+    }
+    if (large) lqs.put((uint32_t)b, sh.bcast[1] + rl, BwtItem{(uint32_t)b, ex, c, 1});
 }
 
-// ---- kernel 2: one wave per queued bucket (any block): sort by the next 8
-// bytes, write SA, BWT bytes and origPtr; groups go to the block's list
+// ---- kernel 2 (one launch per level, all blocks at once): every large
+// segment of the level queue is partitioned by one workgroup.  The last level
+// (`last` != 0) keeps partitioning its segment's large children itself, level
+// by level, up to kMaxDepth.
+__global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                        const uint32_t* __restrict__ lens,
+                                                        uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                        uint32_t* __restrict__ orig_out, uint8_t* scratch,
+                                                        size_t scratch_per_slot, int S, const BwtItem* __restrict__ lin,
+                                                        const uint32_t* __restrict__ lin_count, BwtItem* __restrict__ lout,
+                                                        uint32_t* __restrict__ lout_count, size_t lcap,
+                                                        uint64_t* __restrict__ squeue, uint32_t* __restrict__ scount,
+                                                        size_t scap, Seg* __restrict__ grp_all,
+                                                        uint32_t* __restrict__ ngroups, uint32_t* __restrict__ p2list,
+                                                        uint32_t* __restrict__ p2count, int last) {
+    __shared__ LevelLds L;
+    const uint32_t nin = shard_index_load(lin_count, L.si);
+    if (blockIdx.x >= nin) return;
+    Scratch s = carve(scratch + (size_t)blockIdx.x * scratch_per_slot, S);
+    const int t = threadIdx.x;
+    const Sharded<uint64_t> sq{squeue, scount, scap};
+    for (uint32_t q = blockIdx.x; q < nin; q += gridDim.x) {
+        const BwtItem it = lin[shard_locate(L.si, q, lcap)];
+        const uint32_t b = uniform(it.block);
+        const int n = (int)uniform(lens[b]);
+        const uint8_t* T = blocks + (size_t)b * stride;
+        uint32_t* sa = sa_all + (size_t)b * stride;
+        uint8_t* bw = bwt_out + (size_t)b * stride;
+        const GroupSink sink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu, p2list,
+                             p2count, b, nullptr, nullptr};
+        uint32_t d = uniform(it.depth);
+        if (!last) {
+            partition_segment(T, n, b, sa, Seg{it.start, it.len}, d, L, s.vb, sq,
+                              GlobalLarge{Sharded<BwtItem>{lout, lout_count, lcap}}, sink, bw, orig_out + b);
+            continue;
+        }
+        // local levels: s.large / s.large2 ping-pong, counter in L.sh.cnt[3]
+        if (t == 0) {
+            s.large[0] = Seg{it.start, it.len};
+            L.sh.cnt[1] = 1;
+        }
+        __syncthreads();
+        Seg* cur = s.large;
+        Seg* nxt = s.large2;
+        for (;;) {
+            const uint32_t nc = uniform(L.sh.cnt[1]);
+            if (nc == 0) break;
+            if (t == 0) L.sh.cnt[3] = 0;
+            __syncthreads();
+            for (uint32_t k = 0; k < nc; ++k)
+                partition_segment(T, n, b, sa, cur[k], d, L, s.vb, sq, LocalLarge{nxt, &L.sh.cnt[3]}, sink, bw,
+                                  orig_out + b);
+            if (t == 0) L.sh.cnt[1] = L.sh.cnt[3];
+            __syncthreads();
+            Seg* tmp = cur;
+            cur = nxt;
+            nxt = tmp;
+            d++;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- kernel 3: one wave per queued batch of small segments (any block, any
+// depth): sort, write SA, BWT bytes and origPtr; tie groups go to the
+// block's tie list for the tie rounds
 __global__ __launch_bounds__(256) void bwt_small_kernel(const uint8_t* __restrict__ blocks, size_t stride,
                                                         const uint32_t* __restrict__ lens,
                                                         uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
                                                         uint32_t* __restrict__ orig_out,
-                                                        const uint64_t* __restrict__ queue,
-                                                        const uint32_t* __restrict__ qcount, Seg* __restrict__ grp_all,
-                                                        uint32_t* __restrict__ ngroups, uint32_t* __restrict__ p2list,
-                                                        uint32_t* __restrict__ p2count) {
+                                                        const uint64_t* __restrict__ squeue,
+                                                        const uint32_t* __restrict__ scount, size_t scap,
+                                                        uint64_t* __restrict__ tl, uint32_t* __restrict__ tcount,
+                                                        size_t tcap) {
     __shared__ Bucket2Lds lds[NT / 64];
-    const uint32_t nq = uniform(*qcount);
+    __shared__ ShardIndex si;
+    const uint32_t nq = shard_index_load(scount, si);
     const uint32_t nwaves = gridDim.x * (NT / 64);
     for (uint32_t q = blockIdx.x * (NT / 64) + wave_id(); q < nq; q += nwaves) {
-        const uint64_t e = queue[q];
-        const uint32_t b = uniform((uint32_t)(e >> (kQStartBits + kQLenBits)));
-        const Seg seg{(uint32_t)(e >> kQLenBits) & ((1u << kQStartBits) - 1u),
-                      (uint32_t)(e & ((1u << kQLenBits) - 1u)) + 1u};
+        const uint64_t e = squeue[shard_locate(si, uniform(q), scap)];
+        const uint32_t b = uniform((uint32_t)(e >> 42));
+        const Seg seg{uniform((uint32_t)(e >> 22) & 0xfffffu), uniform((uint32_t)(e >> 13) & 511u) + 1u};
+        const uint32_t d = uniform((uint32_t)e & 0x1fffu);
         const int n = (int)uniform(lens[b]);
         Scratch s{};
         s.sa = sa_all + (size_t)b * stride;
-        const GroupSink sink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu, p2list, p2count, b};
-        wave_sort_bucket2(blocks + (size_t)b * stride, n, s, seg, sink, bwt_out + (size_t)b * stride, orig_out + b,
+        const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, b, tl + (size_t)b * tcap, tcount + b};
+        wave_sort_bucket2(blocks + (size_t)b * stride, n, s, seg, d, sink, bwt_out + (size_t)b * stride, orig_out + b,
                           lds[wave_id()]);
     }
 }
 
-// ---- kernel 3: blocks with large first-byte buckets, one workgroup slot
-// each (blocks pulled from a counter): levels of partitions by the next byte
-// and wave sorts of the small children
-__global__ __launch_bounds__(256) void bwt_large_kernel(const uint8_t* __restrict__ blocks, size_t stride,
-                                                        const uint32_t* __restrict__ lens, int nblocks,
-                                                        uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
-                                                        uint32_t* __restrict__ orig_out, uint8_t* scratch,
-                                                        size_t scratch_per_slot, int S,
-                                                        const Seg* __restrict__ large_all,
-                                                        const uint32_t* __restrict__ nlarge,
-                                                        Seg* __restrict__ grp_all, uint32_t* __restrict__ ngroups,
-                                                        uint32_t* __restrict__ p2list, uint32_t* __restrict__ p2count,
-                                                        const uint32_t* __restrict__ clist,
-                                                        const uint32_t* __restrict__ ccount, uint32_t* pull) {
-    __shared__ BwtShared sh;
-    Scratch s = carve(scratch + (size_t)blockIdx.x * scratch_per_slot, S);
-    const int t = threadIdx.x;
-    const uint32_t nw = uniform(*ccount);
-    for (;;) {
-        if (t == 0) sh.bcast[0] = atomicAdd(pull, 1u);
-        __syncthreads();
-        // wave-uniform (SGPR) values keep every branch below uniform; the
-        // barrier closing each iteration keeps the back edge convergent
-        const uint32_t k = uniform(sh.bcast[0]);
-        if (k >= nw) break;
-        const int b = (int)uniform(clist[k]);
-        const int n = (int)uniform(lens[b]);
-        s.sa = sa_all + (size_t)b * stride;
-        const uint32_t nl = uniform(nlarge[b]);
-        for (uint32_t q = t; q < nl; q += NT) s.large[q] = large_all[(size_t)b * 256 + q];
-        if (t < 8) sh.cnt[t] = 0;
-        if (t == 0) sh.cnt[1] = nl;
-        __syncthreads();
-        const GroupSink sink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu, p2list, p2count,
-                             (uint32_t)b};
-        bwt_levels(blocks + (size_t)b * stride, n, bwt_out + (size_t)b * stride, orig_out + b, s, sh, sink,
-                   b == nblocks / 2);
-        __syncthreads();
+// ---- kernel 4 (one launch per round, one workgroup per block): the block's
+// tie groups sorted by their next 8 bytes -- groups of <= kTieThread
+// rotations one per thread, larger ones one per wave.  New ties go to the
+// next round's list; the last round hands them to the block's group list for
+// prefix doubling.
+__global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                      const uint32_t* __restrict__ lens,
+                                                      uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                      uint32_t* __restrict__ orig_out,
+                                                      const uint64_t* __restrict__ tin,
+                                                      const uint32_t* __restrict__ tin_count,
+                                                      uint64_t* __restrict__ tout, uint32_t* __restrict__ tout_count,
+                                                      size_t tcap, Seg* __restrict__ grp_all,
+                                                      uint32_t* __restrict__ ngroups, uint32_t* __restrict__ p2list,
+                                                      uint32_t* __restrict__ p2count, int last) {
+    __shared__ TieLds L;
+    __shared__ uint32_t ocount;
+    const uint32_t b = blockIdx.x;
+    const uint32_t nq = uniform(tin_count[b]);
+    if (nq == 0) {
+        if (threadIdx.x == 0) tout_count[b] = 0;
+        return;
     }
+    if (threadIdx.x == 0) ocount = 0;
+    __syncthreads();
+    const int n = (int)uniform(lens[b]);
+    const uint8_t* T = blocks + (size_t)b * stride;
+    uint32_t* sa = sa_all + (size_t)b * stride;
+    uint8_t* bw = bwt_out + (size_t)b * stride;
+    const uint64_t* in = tin + (size_t)b * tcap;
+    const GroupSink sink = last ? GroupSink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu,
+                                            p2list, p2count, b, nullptr, nullptr}
+                                : GroupSink{nullptr, nullptr, 0, nullptr, nullptr, b, tout + (size_t)b * tcap, &ocount};
+    auto unpack = [](uint64_t e, Seg& seg, uint32_t& d) {
+        seg = Seg{(uint32_t)(e >> 22) & 0xfffffu, ((uint32_t)(e >> 13) & 511u) + 1u};
+        d = (uint32_t)e & 0x1fffu;
+    };
+    // small groups: one per thread
+    for (uint32_t q = threadIdx.x; q < nq; q += NT) {
+        uint32_t d;
+        Seg seg;
+        unpack(in[q], seg, d);
+        if (seg.len <= (uint32_t)kTieThread) thread_sort_ties(T, n, sa, seg, d, sink, bw, orig_out + b, L);
+    }
+    // large groups: one per wave (the list is scanned for them)
+    for (uint32_t q0 = wave_id() * 64; q0 < nq; q0 += NT) {
+        const uint32_t q = q0 + lane_id();
+        uint32_t d = 0;
+        Seg seg{0, 0};
+        if (q < nq) unpack(in[q], seg, d);
+        uint64_t big = __ballot(q < nq && seg.len > (uint32_t)kTieThread);
+        while (big) {
+            const int l = __builtin_ctzll(big);
+            big &= big - 1;
+            const Seg sg{uniform(__shfl(seg.start, l)), uniform(__shfl(seg.len, l))};
+            const uint32_t dd = uniform(__shfl(d, l));
+            Scratch s{};
+            s.sa = sa;
+            wave_sort_any<0>(T, n, s, sg, dd, sink, bw, orig_out + b);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && !last) tout_count[b] = ocount;
 }
 
-// ---- kernel 4: blocks with groups left: labels, prefix doubling, BWT bytes
+// ---- kernel 5: blocks with groups left: labels, prefix doubling, BWT bytes
 __global__ __launch_bounds__(256) void bwt_double_kernel(const uint8_t* __restrict__ blocks, size_t stride,
                                                          const uint32_t* __restrict__ lens, int nblocks,
                                                          uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,

@@ -10,29 +10,43 @@ namespace bz2mi {
 // Scratch bytes one BWT workgroup slot needs for blocks of S bytes.
 inline size_t bwt_slot_bytes(int S) { return (size_t)48 * (size_t)S + 4096; }
 
-// BWT in four launches (bwt.hip): per-block counting sort by the first byte;
-// one wave per small bucket across all blocks; levels of partitions for the
-// blocks with large buckets; prefix doubling for the blocks with groups left.
+// BWT (bwt.hip): per-block counting sort by the first byte; levels of
+// partitions by the next byte for the large buckets of all blocks at once
+// (one launch per level); one wave per small bucket across all blocks; prefix
+// doubling for the blocks with tie groups left.
 struct BwtSeg {
     uint32_t start, len;
 };
+struct BwtItem {
+    uint32_t block, start, len, depth;
+};
+constexpr int kBwtLevels = 4;  // global partition levels (the last one finishes its segments' subtrees)
 __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
-                                  uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint64_t* queue,
-                                  uint32_t* qcount, BwtSeg* large_all, uint32_t* nlarge, uint32_t* ngroups,
-                                  uint32_t* clist, uint32_t* ccount, uint32_t* present_out);
+                                  uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint64_t* squeue,
+                                  uint32_t* scount, size_t scap, BwtItem* lq, uint32_t* lcount, size_t lcap,
+                                  uint32_t* present_out);
+__global__ void bwt_level_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
+                                 uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,
+                                 int S, const BwtItem* lin, const uint32_t* lin_count, BwtItem* lout,
+                                 uint32_t* lout_count, size_t lcap, uint64_t* squeue, uint32_t* scount, size_t scap,
+                                 BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count, int last);
 __global__ void bwt_small_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
-                                 uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* queue,
-                                 const uint32_t* qcount, BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list,
-                                 uint32_t* p2count);
-__global__ void bwt_large_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
-                                 uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch,
-                                 size_t scratch_per_slot, int S, const BwtSeg* large_all, const uint32_t* nlarge,
-                                 BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count,
-                                 const uint32_t* clist, const uint32_t* ccount, uint32_t* pull);
+                                 uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* squeue,
+                                 const uint32_t* scount, size_t scap, uint64_t* tl, uint32_t* tcount, size_t tcap);
+constexpr int kBwtTieRounds = 6;  // rounds of 8 more bytes for tie groups before prefix doubling
+__global__ void bwt_tie_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
+                               uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* tin, const uint32_t* tin_count,
+                               uint64_t* tout, uint32_t* tout_count, size_t tcap, BwtSeg* grp_all,
+                               uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count, int last);
+constexpr int kBwtShards = 64;  // queue shards (bwt.hip kShards)
 __global__ void bwt_double_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                                   uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch,
                                   size_t scratch_per_slot, int S, BwtSeg* grp_all, const uint32_t* ngroups,
                                   const uint32_t* p2list, const uint32_t* p2count, uint32_t* pull);
+// small-queue capacity (entries) per block and level-queue capacity per block
+// (a shard holds the entries of every 64th block)
+__host__ __device__ inline size_t bwt_squeue_per_block(int S) { return (size_t)S / 2 + 2; }
+__host__ __device__ inline size_t bwt_lqueue_per_block(int S) { return (size_t)S / 512 + 2; }
 // per-block group list capacity (BwtSeg entries) for a block stride
 __host__ __device__ inline size_t bwt_group_stride(size_t stride) { return stride / 2 + 2; }
 
