@@ -108,6 +108,8 @@ struct bz2mi_ctx {
     uint64_t* d_tq[2] = {nullptr, nullptr};         // BWT per-block tie-group lists (ping-pong)
     uint32_t* d_tc = nullptr;                       // their per-block counts (2 x blocks)
     int small_grid = 0;                             // resident workgroups of bwt_small_kernel
+    int level_slots = 0;                            // resident workgroups of bwt_level_kernel
+    uint8_t* d_lscratch = nullptr;                  // their scratch slots
     int bwtq_blocks = 0;           // capacity of the queues in blocks
     uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
     uint32_t* d_crctab = nullptr;
@@ -264,8 +266,8 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");
     for (int d = 1; d <= kBwtLevels; ++d) {
-        hipLaunchKernelGGL(bwt_level_kernel, dim3(c->bwt_slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
-                           t.d_sa, t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, c->d_lq[d & 1],
+        hipLaunchKernelGGL(bwt_level_kernel, dim3(c->level_slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
+                           t.d_sa, t.d_bwt, t.d_orig, c->d_lscratch, bwt_level_slot_bytes(c->S), c->S, c->d_lq[d & 1],
                            lcount + d * kBwtShards, c->d_lq[(d + 1) & 1], lcount + (d + 1) * kBwtShards, lcap,
                            c->d_sq, scount, scap, t.d_groups, t.d_ngroups, t.d_p2list, p2count,
                            d == kBwtLevels ? 1 : 0);
@@ -660,9 +662,15 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(bz2mi::bwt_small_kernel),
                                                          256, 0) != hipSuccess || occ < 1)
             occ = 2;
-        c->small_grid = cus * occ;
+        c->small_grid = std::max(8, cus * occ / 8 * 8);  // multiple of 8 (XCD split)
+        occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(bz2mi::bwt_level_kernel),
+                                                         256, 0) != hipSuccess || occ < 1)
+            occ = 4;
+        c->level_slots = std::max(8, cus * occ / 8 * 8);
     }
     if (dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S)) ||
+        dalloc(&c->d_lscratch, c->level_slots * bz2mi::bwt_level_slot_bytes(c->S)) ||
         dalloc(&c->d_state, (size_t)c->p * bz2mi::kMaxAlpha) || dalloc(&c->d_sd, 1) || dalloc(&c->d_vol, 4)) {
         bz2mi_destroy(c);
         return nullptr;
@@ -690,7 +698,7 @@ void bz2mi_destroy(bz2mi_ctx* c) {
     for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB})
         if (st) (void)hipStreamSynchronize(st);
     std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_sq, c->d_lq[0], c->d_lq[1], c->d_tq[0], c->d_tq[1],
-                               c->d_tc, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
+                               c->d_tc, c->d_lscratch, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
                                c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd,
                                c->d_starts, c->d_nb};
     for (const Batch& t : c->sets) {

@@ -778,30 +778,26 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
 constexpr int kTieThread = 16;
 
 struct TieLds {
-    uint64_t key[kTieThread][NT];
-    uint32_t idx[kTieThread][NT];
+    uint64_t key[kTieThread * NT];
+    uint32_t idx[kTieThread * NT];
+    uint32_t off[NT];  // member offset of each thread's group
+    uint32_t gst[NT];  // group start in SA
+    uint32_t gdp[NT];  // group depth
+    uint32_t tmp[NT / 32];
 };
 
-__device__ void thread_sort_ties(const uint8_t* __restrict__ T, int n, uint32_t* __restrict__ sa, Seg seg,
-                                 uint32_t d, const GroupSink& sink, uint8_t* __restrict__ bwt,
-                                 uint32_t* __restrict__ orig, TieLds& L) {
-    const int t = threadIdx.x;
-    for (uint32_t k = 0; k < seg.len; ++k) {
-        const uint32_t i = sa[seg.start + k];
-        uint32_t p = i + d;
-        if (p >= (uint32_t)n) p %= (uint32_t)n;
-        L.key[k][t] = load8(T, n, p);
-        L.idx[k][t] = i;
-    }
+__device__ void thread_rank_ties(const uint8_t* __restrict__ T, int n, uint32_t* __restrict__ sa, Seg seg,
+                                 uint32_t d, uint32_t off, const GroupSink& sink, uint8_t* __restrict__ bwt,
+                                 uint32_t* __restrict__ orig, const TieLds& L) {
     for (uint32_t a = 0; a < seg.len; ++a) {
-        const uint64_t ka = L.key[a][t];
-        const uint32_t ia = L.idx[a][t];
+        const uint64_t ka = L.key[off + a];
+        const uint32_t ia = L.idx[off + a];
         uint32_t lt = 0, le = 0, eqlt = 0;
         for (uint32_t q = 0; q < seg.len; ++q) {
-            const uint64_t kq = L.key[q][t];
+            const uint64_t kq = L.key[off + q];
             lt += kq < ka;
             le += kq <= ka;
-            eqlt += (kq == ka) & (L.idx[q][t] < ia);
+            eqlt += (kq == ka) & (L.idx[off + q] < ia);
         }
         const uint32_t fin = seg.start + lt + eqlt;
         sa[fin] = ia;
@@ -815,6 +811,7 @@ __device__ void thread_sort_ties(const uint8_t* __restrict__ T, int n, uint32_t*
 // counter and capacity, so that the producers of the whole chip do not all
 // hit one atomic counter.  Consumers index the concatenation of the shards.
 constexpr int kShards = 64;
+constexpr uint32_t kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin (grids are multiples of 8)
 
 template <typename Item>
 struct Sharded {
@@ -858,44 +855,109 @@ __device__ __forceinline__ size_t shard_locate(const ShardIndex& si, uint32_t q,
 }
 
 // Pack the children of a partition (counts in sh.hist, in byte order from
-// relative position 0) into batches for the small kernel: runs of
-// consecutive children of <= kSmall rotations, at most kSmall rotations per
-// batch, large children break runs.  A batch of one child is sorted from
-// depth d+1, a batch of several from depth d (byte d separates them).
-// Batches with no child of >= 2 rotations are dropped (singletons are final).
-// Thread 0 packs; returns the batch count (sh.bat_*).
+// relative position 0) into batches for the small kernel.  Children of
+// > kSmall rotations (partitioned further) and of > kSmall/2 (a batch of
+// their own) break runs; inside a run, the children of <= kSmall/2 whose
+// run-relative start lies in the same 256-rotation window form one batch
+// (so a batch holds < kSmall rotations and never splits a child).  A batch of
+// one child is sorted from depth d+1, a batch of several from depth d (byte
+// d separates them).  Batches with no child of >= 2 rotations are dropped
+// (singletons are final).  Wave 0 packs with wave scans (4 children per
+// lane); returns the batch count (sh.bat_*).
 __device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
-    if (threadIdx.x == 0) {
-        uint32_t nb = 0, pos = 0, bs = 0, bl = 0, nch = 0;
-        bool useful = false;
-        for (int c = 0; c < 256; ++c) {
-            const uint32_t m = sh.hist[c];
-            if (m == 0) continue;
-            const bool big = m > (uint32_t)kSmall;
-            if (bl && (big || bl + m > (uint32_t)kSmall)) {
-                if (useful) {
-                    sh.bat_start[nb] = bs;
-                    sh.bat_len[nb] = bl | (nch == 1 ? 0x80000000u : 0u);
-                    nb++;
-                }
-                bl = 0;
-                nch = 0;
-                useful = false;
-            }
-            if (!big) {
-                if (bl == 0) bs = pos;
-                bl += m;
-                nch++;
-                useful |= m > 1;
-            }
-            pos += m;
+    if (threadIdx.x < 64) {
+        const int lane = lane_id();
+        constexpr uint32_t kHalf = kSmall / 2;
+        uint32_t m[4], pos[4], sinc[4], brk[4];
+        uint32_t tot = 0, stot = 0, btot = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            m[j] = sh.hist[lane * 4 + j];
+            pos[j] = tot;
+            tot += m[j];
+            const bool small = m[j] > 0 && m[j] <= kHalf;
+            stot += small ? m[j] : 0u;
+            sinc[j] = stot;
+            brk[j] = m[j] > kHalf;
+            btot += brk[j];
         }
-        if (bl && useful) {
-            sh.bat_start[nb] = bs;
-            sh.bat_len[nb] = bl | (nch == 1 ? 0x80000000u : 0u);
-            nb++;
+        // child start positions, small-size prefix, breaker count (run id)
+        const uint32_t pos_ex = wave_incl_sum(tot) - tot;
+        const uint32_t s_ex = wave_incl_sum(stot) - stot;
+        const uint32_t b_ex = wave_incl_sum(btot) - btot;
+        // S at the last breaker (inclusive): max-scan (S is nondecreasing)
+        uint32_t lastb = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (brk[j]) lastb = s_ex + sinc[j];
+        const uint32_t base_in = lane_prev(wave_incl_max(lastb), 0u);
+        uint32_t key[4], run = b_ex, base = base_in, kmax = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool small = m[j] > 0 && m[j] <= kHalf;
+            if (brk[j]) {
+                run++;
+                base = s_ex + sinc[j];
+            }
+            const uint32_t P = s_ex + sinc[j] - (small ? m[j] : 0u) - base;  // run-relative start
+            key[j] = small ? (run << 12) + (P >> 8) + 1u : 0u;  // P < 2^20: P >> 8 < 4096
+            kmax = key[j] > kmax ? key[j] : kmax;
         }
-        sh.cnt[7] = nb;
+        uint32_t prevk = lane_prev(wave_incl_max(kmax), 0u);
+        uint32_t st[4], nst = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool mid = m[j] > kHalf && m[j] <= (uint32_t)kSmall;
+            st[j] = (key[j] && key[j] != prevk) || mid;
+            if (key[j]) prevk = key[j];
+            nst += st[j];
+        }
+        const uint32_t st_ex = wave_incl_sum(nst) - nst;
+        const uint32_t nbat = (uint32_t)__builtin_amdgcn_readlane((int)(st_ex + nst), 63);
+        // per batch: start, length, children, any child of >= 2
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sh.wcnt[0][lane * 4 + j] = 0;  // length
+            sh.wcnt[1][lane * 4 + j] = 0;  // children | useful << 16
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t idx = st_ex;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool member = key[j] || (m[j] > kHalf && m[j] <= (uint32_t)kSmall);
+            if (st[j]) {
+                sh.bat_start[idx] = pos_ex + pos[j];
+                idx++;
+            }
+            if (member) {
+                atomicAdd(&sh.wcnt[0][idx - 1], m[j]);
+                atomicAdd(&sh.wcnt[1][idx - 1], 1u | (m[j] >= 2 ? 0x10000u : 0u));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // keep the useful batches (compaction, 4 per lane)
+        uint32_t keep[4], nk = 0, bs[4], bl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = (uint32_t)(lane * 4 + j);
+            const uint32_t ch = sh.wcnt[1][k];
+            keep[j] = k < nbat && (ch >> 16) != 0;
+            bs[j] = sh.bat_start[k];
+            bl[j] = sh.wcnt[0][k] | ((ch & 0xffffu) == 1 ? 0x80000000u : 0u);
+            nk += keep[j];
+        }
+        const uint32_t k_ex = wave_incl_sum(nk) - nk;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t o = k_ex;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (keep[j]) {
+                sh.bat_start[o] = bs[j];
+                sh.bat_len[o] = bl[j];
+                o++;
+            }
+        }
+        if (lane == 63) sh.cnt[7] = k_ex + nk;
     }
     __syncthreads();
     return uniform(sh.cnt[7]);
@@ -906,7 +968,7 @@ __device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
 // ones go to the small queue as batches, larger ones to `large_out` or, at
 // the depth limit, to the group sink.  The segment is staged in LDS
 // (`stage`, kStage entries) or, when longer, in the global `spill` area.
-constexpr int kStage = 6144;
+constexpr int kStage = 2048;
 
 struct LevelLds {
     BwtShared sh;
@@ -914,36 +976,94 @@ struct LevelLds {
     uint32_t stage[kStage];
 };
 
+// PHASES builds: per-phase wall-clock sums of partition_segment (thread 0 of
+// every workgroup), added to g_bwt_phase[8..13] at the end of the kernel
+struct PartTimes {
+    unsigned long long acc[6];
+};
+#ifdef BZ2MI_PHASES
+#define PT_MARK(pt, k, last)                          \
+    do {                                              \
+        if (threadIdx.x == 0) {                       \
+            const unsigned long long now_ = wall_clock64(); \
+            (pt).acc[k] += now_ - (last);             \
+            (last) = now_;                            \
+        }                                             \
+    } while (0)
+#else
+#define PT_MARK(pt, k, last) \
+    do {                     \
+    } while (0)
+#endif
+
 template <typename LargeOut>
 __device__ void partition_segment(const uint8_t* __restrict__ T, int n, uint32_t b, uint32_t* __restrict__ sa,
                                   Seg seg, uint32_t d, LevelLds& L, uint32_t* __restrict__ spill,
                                   const Sharded<uint64_t>& sq, const LargeOut& large_out, const GroupSink& sink,
-                                  uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig) {
+                                  uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig, PartTimes& pt) {
     BwtShared& sh = L.sh;
+    unsigned long long last_t = 0;
+#ifdef BZ2MI_PHASES
+    last_t = wall_clock64();
+#endif
     seg.start = uniform(seg.start);
     seg.len = uniform(seg.len);
     const int t = threadIdx.x;
     uint32_t* cp = seg.len <= (uint32_t)kStage ? L.stage : spill;
     sh.hist[t] = 0;
     __syncthreads();
-    for (uint32_t k = t; k < seg.len; k += NT) {
-        const uint32_t i = sa[seg.start + k];
-        cp[k] = i;
-        atomicAdd(&sh.hist[byte_at(T, n, i + d)], 1u);
+    // staged: rotation index | byte d << 24 (indices < 2^20).  The LDS
+    // counters take one atomic per distinct byte of a wave (text is skewed:
+    // plain atomics would serialise on the frequent letters).
+    // 8 rotations per thread and step: all SA loads, then all byte gathers,
+    // are in flight together (one memory latency per step, not per rotation)
+    constexpr int U = 8;
+    const uint32_t rounds = (seg.len + NT - 1) / NT;
+    for (uint32_t r0 = 0; r0 < rounds; r0 += U) {
+        uint32_t iv[U], cv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t k = (r0 + j) * NT + t;
+            iv[j] = k < seg.len ? sa[seg.start + k] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t k = (r0 + j) * NT + t;
+            cv[j] = k < seg.len ? byte_at(T, n, iv[j] + d) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t k = (r0 + j) * NT + t;
+            const bool v = k < seg.len;
+            if (v) cp[k] = iv[j] | (cv[j] << 24);
+            const uint64_t peers = wave_match8(cv[j], v);
+            if (v && (peers & __lanemask_lt()) == 0) atomicAdd(&sh.hist[cv[j]], (uint32_t)__popcll(peers));
+        }
     }
     __syncthreads();
+    PT_MARK(pt, 0, last_t);
     const uint32_t c = sh.hist[t];
     uint32_t total;
     const uint32_t ex = wg_excl_sum<NT>(c, sh.tmp, &total);
     sh.base[t] = ex;
     __syncthreads();
     // stable placement is not needed: later sorts break ties by index
-    for (uint32_t k = t; k < seg.len; k += NT) {
-        const uint32_t i = cp[k];
-        const uint32_t slot = atomicAdd(&sh.base[byte_at(T, n, i + d)], 1u);
-        sa[seg.start + slot] = i;
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t k = r * NT + t;
+        const bool v = k < seg.len;
+        const uint32_t x = v ? cp[k] : 0u;
+        const uint32_t cc = x >> 24;
+        const uint64_t peers = wave_match8(cc, v);
+        const uint64_t below = peers & __lanemask_lt();
+        const int leader = peers ? __builtin_ctzll(peers) : 0;
+        uint32_t base = 0;
+        if (v && below == 0) base = atomicAdd(&sh.base[cc], (uint32_t)__popcll(peers));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (v) sa[seg.start + base + (uint32_t)__popcll(below)] = x & 0xffffffu;
     }
+    PT_MARK(pt, 1, last_t);
     const uint32_t nbat = pack_children(sh);
+    PT_MARK(pt, 2, last_t);
     // large children: one reservation per workgroup
     const bool deep = c > (uint32_t)kSmall && d + 1 >= (uint32_t)kMaxDepth;
     const bool large = c > (uint32_t)kSmall && !deep;
@@ -954,6 +1074,7 @@ __device__ void partition_segment(const uint8_t* __restrict__ T, int n, uint32_t
         sh.bcast[2] = nl ? large_out.reserve(b, nl) : 0u;
     }
     __syncthreads();  // also orders the SA scatter before the final reads
+    PT_MARK(pt, 3, last_t);
     if (c == 1) {
         const uint32_t i = sa[seg.start + ex];
         bwt[seg.start + ex] = bwt_byte(T, n, i);
@@ -969,6 +1090,7 @@ __device__ void partition_segment(const uint8_t* __restrict__ T, int n, uint32_t
         sq.put(b, sh.bcast[1] + t, sq_pack(b, seg.start + sh.bat_start[t], bl & 0x7fffffffu, d + one));
     }
     __syncthreads();
+    PT_MARK(pt, 4, last_t);
 }
 
 // next-level queue (global, all blocks) or the workgroup's own list
@@ -1061,11 +1183,30 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
                                                         uint32_t* __restrict__ p2count, int last) {
     __shared__ LevelLds L;
     const uint32_t nin = shard_index_load(lin_count, L.si);
-    if (blockIdx.x >= nin) return;
-    Scratch s = carve(scratch + (size_t)blockIdx.x * scratch_per_slot, S);
+    if (nin == 0) return;
+    // slot scratch (bwt_level_slot_bytes): spill area, then the local lists
+    Scratch s{};
+    {
+        uint8_t* p = scratch + (size_t)blockIdx.x * scratch_per_slot;
+        s.vb = (uint32_t*)p;
+        p += 4 * (size_t)S;
+        s.large = (Seg*)p;
+        p += 8 * ((size_t)S / kSmall + 8);
+        s.large2 = (Seg*)p;
+    }
     const int t = threadIdx.x;
     const Sharded<uint64_t> sq{squeue, scount, scap};
-    for (uint32_t q = blockIdx.x; q < nin; q += gridDim.x) {
+    PartTimes pt{};
+    unsigned long long item_t = 0;
+    // XCD-aware: workgroups are dealt to the 8 XCDs round-robin; XCD x takes
+    // the x-th eighth of the queue, so the segments (and blocks) one XCD
+    // works on at a time are neighbours and stay in its L2
+    const uint32_t xcd = blockIdx.x % kXcds, nloc = gridDim.x / kXcds;
+    const uint32_t qlo = (uint32_t)((uint64_t)nin * xcd / kXcds), qhi = (uint32_t)((uint64_t)nin * (xcd + 1) / kXcds);
+    for (uint32_t q = qlo + blockIdx.x / kXcds; q < qhi; q += nloc) {
+#ifdef BZ2MI_PHASES
+        item_t = wall_clock64();
+#endif
         const BwtItem it = lin[shard_locate(L.si, q, lcap)];
         const uint32_t b = uniform(it.block);
         const int n = (int)uniform(lens[b]);
@@ -1077,7 +1218,7 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
         uint32_t d = uniform(it.depth);
         if (!last) {
             partition_segment(T, n, b, sa, Seg{it.start, it.len}, d, L, s.vb, sq,
-                              GlobalLarge{Sharded<BwtItem>{lout, lout_count, lcap}}, sink, bw, orig_out + b);
+                              GlobalLarge{Sharded<BwtItem>{lout, lout_count, lcap}}, sink, bw, orig_out + b, pt);
             continue;
         }
         // local levels: s.large / s.large2 ping-pong, counter in L.sh.cnt[3]
@@ -1095,7 +1236,7 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
             __syncthreads();
             for (uint32_t k = 0; k < nc; ++k)
                 partition_segment(T, n, b, sa, cur[k], d, L, s.vb, sq, LocalLarge{nxt, &L.sh.cnt[3]}, sink, bw,
-                                  orig_out + b);
+                                  orig_out + b, pt);
             if (t == 0) L.sh.cnt[1] = L.sh.cnt[3];
             __syncthreads();
             Seg* tmp = cur;
@@ -1105,12 +1246,19 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
         }
         __syncthreads();
     }
+#ifdef BZ2MI_PHASES
+    if (t == 0) {
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_bwt_phase[8 + k], pt.acc[k]);
+        atomicAdd(&g_bwt_phase[14], 1ull);
+    }
+#endif
+    (void)item_t;
 }
 
 // ---- kernel 3: one wave per queued batch of small segments (any block, any
 // depth): sort, write SA, BWT bytes and origPtr; tie groups go to the
 // block's tie list for the tie rounds
-__global__ __launch_bounds__(256) void bwt_small_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+__global__ __launch_bounds__(256, 4) void bwt_small_kernel(const uint8_t* __restrict__ blocks, size_t stride,
                                                         const uint32_t* __restrict__ lens,
                                                         uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
                                                         uint32_t* __restrict__ orig_out,
@@ -1121,8 +1269,10 @@ __global__ __launch_bounds__(256) void bwt_small_kernel(const uint8_t* __restric
     __shared__ Bucket2Lds lds[NT / 64];
     __shared__ ShardIndex si;
     const uint32_t nq = shard_index_load(scount, si);
-    const uint32_t nwaves = gridDim.x * (NT / 64);
-    for (uint32_t q = blockIdx.x * (NT / 64) + wave_id(); q < nq; q += nwaves) {
+    // XCD-aware split of the queue (see bwt_level_kernel)
+    const uint32_t xcd = blockIdx.x % kXcds, nwaves = gridDim.x / kXcds * (NT / 64);
+    const uint32_t qlo = (uint32_t)((uint64_t)nq * xcd / kXcds), qhi = (uint32_t)((uint64_t)nq * (xcd + 1) / kXcds);
+    for (uint32_t q = qlo + blockIdx.x / kXcds * (NT / 64) + wave_id(); q < qhi; q += nwaves) {
         const uint64_t e = squeue[shard_locate(si, uniform(q), scap)];
         const uint32_t b = uniform((uint32_t)(e >> 42));
         const Seg seg{uniform((uint32_t)(e >> 22) & 0xfffffu), uniform((uint32_t)(e >> 13) & 511u) + 1u};
@@ -1173,12 +1323,59 @@ __global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict_
         seg = Seg{(uint32_t)(e >> 22) & 0xfffffu, ((uint32_t)(e >> 13) & 511u) + 1u};
         d = (uint32_t)e & 0x1fffu;
     };
-    // small groups: one per thread
-    for (uint32_t q = threadIdx.x; q < nq; q += NT) {
-        uint32_t d;
-        Seg seg;
-        unpack(in[q], seg, d);
-        if (seg.len <= (uint32_t)kTieThread) thread_sort_ties(T, n, sa, seg, d, sink, bw, orig_out + b, L);
+    // small groups: one per thread, 256 at a time; their members are loaded
+    // by all threads at once (flattened) into LDS, then every thread ranks
+    // its own group there
+    for (uint32_t q0 = 0; q0 < nq; q0 += NT) {
+        const uint32_t q = q0 + threadIdx.x;
+        uint32_t d = 0;
+        Seg seg{0, 0};
+        if (q < nq) unpack(in[q], seg, d);
+        const uint32_t len = seg.len <= (uint32_t)kTieThread ? seg.len : 0u;
+        uint32_t total;
+        const uint32_t off = wg_excl_sum<NT>(len, L.tmp, &total);
+        L.off[threadIdx.x] = off;
+        L.gst[threadIdx.x] = seg.start;
+        L.gdp[threadIdx.x] = d;
+        __syncthreads();
+        // 4 members per thread and step, their loads in flight together
+        for (uint32_t m0 = 0; m0 < total; m0 += 4 * NT) {
+            uint32_t pos[4], dep[4], iv[4];
+            uint64_t kv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t m = m0 + j * NT + threadIdx.x;
+                // owner group: the last g with off[g] <= m
+                uint32_t lo = 0, hi = NT;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (L.off[mid] <= m) lo = mid;
+                    else hi = mid;
+                }
+                pos[j] = L.gst[lo] + (m - L.off[lo]);
+                dep[j] = L.gdp[lo];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) iv[j] = m0 + j * NT + threadIdx.x < total ? sa[pos[j]] : 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t p = iv[j] + dep[j];
+                if (p >= (uint32_t)n) p %= (uint32_t)n;
+                kv[j] = m0 + j * NT + threadIdx.x < total ? load8(T, n, p) : 0ull;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t m = m0 + j * NT + threadIdx.x;
+                if (m < total) {
+                    L.key[m] = kv[j];
+                    L.idx[m] = iv[j];
+                }
+            }
+        }
+        __syncthreads();
+        if (len) thread_rank_ties(T, n, sa, seg, d, off, sink, bw, orig_out + b, L);
+        __syncthreads();
     }
     // large groups: one per wave (the list is scanned for them)
     for (uint32_t q0 = wave_id() * 64; q0 < nq; q0 += NT) {

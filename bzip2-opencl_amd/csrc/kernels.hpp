@@ -9,6 +9,8 @@ namespace bz2mi {
 
 // Scratch bytes one BWT workgroup slot needs for blocks of S bytes.
 inline size_t bwt_slot_bytes(int S) { return (size_t)48 * (size_t)S + 4096; }
+// ... and one bwt_level_kernel workgroup slot (spill area + two segment lists)
+inline size_t bwt_level_slot_bytes(int S) { return (size_t)4 * (size_t)S + 16 * ((size_t)S / 512 + 8) + 256; }
 
 // BWT (bwt.hip): per-block counting sort by the first byte; levels of
 // partitions by the next byte for the large buckets of all blocks at once
