@@ -101,6 +101,9 @@ def main():
     ap.add_argument("--cpu-sample-mib", type=int, default=96)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--mode", choices=["compress", "decompress"], default="compress",
+                    help="compress = the bench line (BASELINE metric); decompress = configs[4]: device "
+                         "decompression of the stream this run compresses (output MB/s)")
     ap.add_argument("--data", choices=["random", "text", "mixed"], default="random",
                     help="random = C2 (the bench line); text = C3 stand-in (seeded word Markov text, enwik9 is "
                          "not available offline); mixed = C4 (rotating random/text/runs/ACGT segments)")
@@ -138,6 +141,9 @@ def main():
 
     def step():
         return ctx.compress_device(x.data_ptr(), n, out.data_ptr(), cap)
+
+    if args.mode == "decompress":
+        return bench_decompress(args, ctx, x, n, out, cap, world, rank, dev)
 
     for _ in range(args.warmup):
         out_len = step()
@@ -213,6 +219,52 @@ def main():
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_decompress(args, ctx, x, n, out, cap, world, rank, dev):
+    """configs[4]: decompression on the device of the .bz2 this run produced
+    (bz2mi's own stream: the reference decoder's block-size limit).
+    One step = the whole stream decoded (candidate scan, Huffman/MTF/RLE2,
+    inverse BWT, RLE1 + CRC checks); value = decompressed MB/s."""
+    import torch
+    import torch.distributed as dist
+    import bz2mi
+    zlen = ctx.compress_device(x.data_ptr(), n, out.data_ptr(), cap)
+    y = torch.empty(n, dtype=torch.uint8, device=dev)
+    d = bz2mi.Decompressor(args.unit)
+    for _ in range(args.warmup):
+        d.decompress_device(out.data_ptr(), zlen, y.data_ptr(), n)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    stage = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = d.decompress_device(out.data_ptr(), zlen, y.data_ptr(), n)
+        for k, v in d.timings().items():
+            stage[k] = stage.get(k, 0.0) + v
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ok = bool(got == n and torch.equal(x, y))
+    if rank == 0:
+        line = {
+            "metric": "decompress MB/s (.bz2 from this run, -9), output bytes", "value": round(world * n * args.steps / dt / 1e6, 2),
+            "unit": "MB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "configs[4] stand-in: " + WORKLOADS[args.data].format(mib=args.mib),
+                       "compressed_bytes": int(zlen), "round_trip_equal": ok},
+            "stage_ms": {k: round(v / args.steps, 3) for k, v in stage.items()},
+        }
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -24,13 +24,15 @@ BZ2MI_EINVAL = -1
 BZ2MI_EDEVICE = -2
 BZ2MI_ESPACE = -3
 BZ2MI_ESTATE = -4
+BZ2MI_EFORMAT = -5
 
 # every symbol include/bz2mi.h declares
 EXPORTS = (
     "bz2mi_last_error", "bz2mi_device_count", "bz2mi_version", "bz2mi_create", "bz2mi_destroy",
     "bz2mi_compress_bound", "bz2mi_compress_rle1", "bz2mi_finish", "bz2mi_compress_blocks",
     "bz2mi_compress", "bz2mi_compress_device", "bz2mi_last_timings", "bz2mi_blocks_done",
-    "bz2mi_last_stats",
+    "bz2mi_last_stats", "bz2mi_dcreate", "bz2mi_ddestroy", "bz2mi_decompress", "bz2mi_decompress_device",
+    "bz2mi_dlast_timings",
 )
 
 _lib = None
@@ -75,6 +77,17 @@ def lib() -> ctypes.CDLL:
     L.bz2mi_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
     L.bz2mi_blocks_done.restype = c.c_uint64
     L.bz2mi_blocks_done.argtypes = [c.c_void_p]
+    L.bz2mi_dcreate.restype = c.c_void_p
+    L.bz2mi_dcreate.argtypes = [c.c_int, c.c_int]
+    L.bz2mi_ddestroy.argtypes = [c.c_void_p]
+    L.bz2mi_decompress.restype = c.c_int
+    L.bz2mi_decompress.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
+                                   c.POINTER(c.c_size_t)]
+    L.bz2mi_decompress_device.restype = c.c_int
+    L.bz2mi_decompress_device.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
+                                          c.POINTER(c.c_size_t), c.c_void_p]
+    L.bz2mi_dlast_timings.restype = c.c_int
+    L.bz2mi_dlast_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
     # debugging entry points (not in include/bz2mi.h)
     L.bz2mi_debug_selftest.restype = c.c_int
     L.bz2mi_debug_selftest.argtypes = [c.POINTER(c.c_uint32), c.c_int]
@@ -193,6 +206,90 @@ class Context:
         arr = (ctypes.c_float * 6)()
         _check(lib().bz2mi_last_timings(self._h, arr))
         return dict(zip(("front", "bwt", "mtf", "seed", "huffman", "assemble"), list(arr)))
+
+
+class DecompressError(RuntimeError):
+    """Corrupt .bz2 data: the reference's std::runtime_error (its message)."""
+
+
+class Decompressor:
+    """A bz2mi_dctx: device decoder of .bz2 streams (the reference's
+    InputStream / BlockDecompressor / HuffmanStageDecoder, InputStream.hpp:36-159).
+    `unit` 10000 accepts the reference's block sizes, 100000 stock bzip2 files."""
+
+    def __init__(self, unit: int = 10000, device: int = 0):
+        L = lib()
+        h = L.bz2mi_dcreate(unit, device)
+        if not h:
+            msg = L.bz2mi_last_error().decode(errors="replace")
+            raise (ValueError if "Invalid" in msg else RuntimeError)(msg)
+        self._h = h
+        self.unit = unit
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().bz2mi_ddestroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @staticmethod
+    def _raise(rc: int) -> None:
+        msg = lib().bz2mi_last_error().decode(errors="replace")
+        if rc == BZ2MI_EFORMAT:
+            raise DecompressError(msg)
+        _check(rc)
+
+    def decompress(self, data, cap: int | None = None) -> bytes:
+        """Host bytes in, host bytes out (the buffer grows once if too small)."""
+        import numpy as np
+        src = np.frombuffer(bytes(data), dtype=np.uint8)
+        cap = cap if cap is not None else max(1 << 16, src.size * 8)
+        for _ in range(2):
+            out = np.empty(max(cap, 1), dtype=np.uint8)
+            n = ctypes.c_size_t(0)
+            rc = lib().bz2mi_decompress(self._h, src.ctypes.data if src.size else None, src.size,
+                                        out.ctypes.data, cap, ctypes.byref(n))
+            if rc == BZ2MI_ESPACE:
+                cap = n.value
+                continue
+            if rc != BZ2MI_OK:
+                self._raise(rc)
+            return out[: n.value].tobytes()
+        raise RuntimeError("decompress: output size changed between attempts")
+
+    def decompress_device(self, d_in_ptr: int, n: int, d_out_ptr: int, cap: int, stream: int = 0) -> int:
+        """Device buffers; returns the decompressed size (raises on errors;
+        on a short buffer RuntimeError names the size needed)."""
+        out_len = ctypes.c_size_t(0)
+        rc = lib().bz2mi_decompress_device(self._h, d_in_ptr, n, d_out_ptr, cap, ctypes.byref(out_len),
+                                           stream or None)
+        if rc == BZ2MI_ESPACE:
+            raise RuntimeError(f"output buffer too small: {out_len.value} bytes needed")
+        if rc != BZ2MI_OK:
+            self._raise(rc)
+        return out_len.value
+
+    def timings(self):
+        arr = (ctypes.c_float * 5)()
+        _check(lib().bz2mi_dlast_timings(self._h, arr))
+        return dict(zip(("scan", "huffman", "ibwt", "rle1", "total"), list(arr)))
+
+
+def decompress(data, unit: int = 10000, device: int = 0) -> bytes:
+    """Whole .bz2 (one or more streams) -> bytes, decoded on the device."""
+    with Decompressor(unit, device) as d:
+        return d.decompress(data)
 
 
 def compress(data, level: int = 9, parallel: int = 10, unit: int = 10000, device: int = 0) -> bytes:

@@ -24,6 +24,13 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+}  // namespace
+
+// shared with the decoder's host code (dapi.hip)
+int bz2mi_set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+namespace {
+
 #define HIPCHECK(expr)                                                                        \
     do {                                                                                      \
         hipError_t e_ = (expr);                                                               \

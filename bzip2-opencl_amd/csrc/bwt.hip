@@ -1002,7 +1002,7 @@ __device__ void partition_segment(const uint8_t* __restrict__ T, int n, uint32_t
                                   const Sharded<uint64_t>& sq, const LargeOut& large_out, const GroupSink& sink,
                                   uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig, PartTimes& pt) {
     BwtShared& sh = L.sh;
-    unsigned long long last_t = 0;
+    [[maybe_unused]] unsigned long long last_t = 0;
 #ifdef BZ2MI_PHASES
     last_t = wall_clock64();
 #endif

@@ -1,0 +1,780 @@
+// bzip2 decompression on the device.
+//
+// Replaces the reference's host decoder: InputStream (include/InputStream.hpp:
+// 36-159: stream header, block / end-of-stream markers, stream CRC),
+// BlockDecompressor (BlockDecompressor.hpp:37-282: block header, symbol map,
+// selectors, table code lengths, Huffman + MTF + RLE2 decode, inverse BWT,
+// RLE1 expansion with the block CRC) and HuffmanStageDecoder
+// (HuffmanStageDecoder.hpp:30-136: canonical code tables, 50-symbol groups).
+// The reference decodes one byte at a time on one thread; here every block of
+// the stream is decoded at once:
+//
+//   K1 dec_scan_kernel     every bit position is tested for the 48-bit block
+//                          and end-of-stream magics (candidates; the 32 bits
+//                          after a magic are the stored CRC)
+//   K2 dec_huff_kernel     one wave per candidate block: header, tables, then
+//                          the Huffman symbols (scalar bit reader, LDS lookup
+//                          tables) with the move-to-front list held across
+//                          the wave (4 entries per lane) and RLE2 runs, giving
+//                          the BWT bytes, their histogram and the end bit
+//   (host)                 the chain stream header -> blocks -> end marker is
+//                          walked over the candidates' end bits, which drops
+//                          magics that occur inside compressed data
+//   K3 dec_ibwt_kernel     one workgroup per block: stable counting sort into
+//                          the merged pointer vector (BlockDecompressor.hpp:
+//                          238-262), then 1024 walkers split the LF cycle into
+//                          segments, a chain pass orders them, and the walkers
+//                          write the RLE1 bytes
+//   K4 dec_rle1_kernel     one workgroup per block, 256 chunks: the RLE1 state
+//                          machine (BlockDecompressor.hpp:55-88) is run from
+//                          all 5 entry states per chunk, chained, then run
+//                          again writing the output; the block CRC is
+//                          combined from the chunk CRCs with x^(8L) mod P.
+#include "common.hpp"
+#include "decode.hpp"
+
+namespace bz2mi {
+
+// x^(8 * 2^k) mod P (CRC32 polynomial 0x04c11db7, MSB-first register)
+__constant__ uint32_t c_xpow8[64];
+
+namespace {
+
+__device__ __forceinline__ uint32_t gf_mulmod(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll 4
+    for (int i = 31; i >= 0; --i) {
+        r = (r << 1) ^ ((r >> 31) ? 0x04c11db7u : 0u);
+        if ((b >> i) & 1u) r ^= a;
+    }
+    return r;
+}
+
+// v * x^(8 L) mod P: the CRC register after L more zero bytes
+__device__ __forceinline__ uint32_t crc_shift(uint32_t v, uint64_t L) {
+    for (int k = 0; L; ++k, L >>= 1)
+        if (L & 1) v = gf_mulmod(v, c_xpow8[k]);
+    return v;
+}
+
+// ---- big-endian bit reader over the compressed stream, all-uniform (one
+// reader per wave; the state lives in SGPRs)
+struct BitReader {
+    const uint32_t* w;  // stream as 32-bit words (byte-swapped on use)
+    uint64_t nbits;     // stream length in bits
+    uint64_t pos;       // next bit (absolute)
+    uint64_t buf;       // MSB-aligned pending bits
+    int nb;             // valid bits in buf
+    uint64_t wnext;     // next word to load
+    bool over;          // read past the end
+
+    __device__ __forceinline__ uint32_t word(uint64_t i) const {
+        // big-endian word i; bytes past the end read as zero (no over-read)
+        const uint64_t nbytes = nbits >> 3;
+        if ((i + 1) * 4 <= nbytes) return __builtin_bswap32(w[i]);
+        uint32_t x = 0;
+        const uint8_t* b = reinterpret_cast<const uint8_t*>(w);
+        for (int q = 0; q < 4; ++q) x = (x << 8) | ((i * 4 + q < nbytes) ? b[i * 4 + q] : 0u);
+        return x;
+    }
+    __device__ void init(const uint8_t* base, uint64_t nbytes, uint64_t bitpos) {
+        // `base` is 4-byte aligned; the tail word may be partial (masked by nbits)
+        w = reinterpret_cast<const uint32_t*>(base);
+        nbits = nbytes * 8;
+        pos = bitpos;
+        wnext = bitpos >> 5;
+        const int off = (int)(bitpos & 31);
+        buf = 0;
+        nb = 0;
+        over = false;
+        refill();
+        buf <<= off;
+        nb -= off;
+    }
+    __device__ __forceinline__ void refill() {
+        while (nb <= 32) {
+            const uint32_t x = word(wnext);
+            buf |= (uint64_t)x << (32 - nb);
+            nb += 32;
+            wnext++;
+        }
+    }
+    __device__ __forceinline__ uint32_t peek(int k) const { return (uint32_t)(buf >> (64 - k)); }
+    __device__ __forceinline__ void skip(int k) {
+        buf <<= k;
+        nb -= k;
+        pos += k;
+        if (pos > nbits) over = true;
+        if (nb <= 32) refill();
+    }
+    __device__ __forceinline__ uint32_t bits(int k) {  // 1..32
+        const uint32_t v = peek(k);
+        skip(k);
+        return v;
+    }
+    __device__ __forceinline__ uint32_t bit() { return bits(1); }
+};
+
+constexpr int kLutBits = 9;
+constexpr uint16_t kLong = 0xffff;
+constexpr int kMaxDecLen = 23;  // HUFFMAN_DECODE_MAXIMUM_CODE_LENGTH (Config.hpp:38)
+constexpr int kDecMaxSel = 18002; // 900 KB blocks (bzip2's BZ_MAX_SELECTORS)
+
+struct HuffLds {
+    uint16_t lut[kMaxTables][1 << kLutBits];  // sym | len << 12, or kLong
+    int32_t limit[kMaxTables][kMaxDecLen + 2];
+    int32_t base[kMaxTables][kMaxDecLen + 2];  // rank of the first code of a length minus that code
+    uint16_t perm[kMaxTables][kMaxAlpha];       // symbols by (length, symbol)
+    uint8_t len[kMaxTables][kMaxAlpha];
+    uint32_t hist[256];
+    uint8_t symmap[256];
+    uint32_t sel[(kDecMaxSel + 7) / 8];  // selectors, 4 bits each
+};
+
+__device__ __forceinline__ void fail(DecBlockInfo* info, uint32_t code) {
+    if (threadIdx.x == 0) info->status = code;
+}
+
+}  // namespace
+
+// ---- K1: candidates.  Thread per 8-byte word of the stream: the 64 bit
+// positions starting in it, the 48-bit window read from 16 bytes.
+__global__ __launch_bounds__(256) void dec_scan_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                       DecCand* __restrict__ cand, uint32_t* __restrict__ ncand,
+                                                       uint32_t cap) {
+    const uint64_t wi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t b0 = wi * 8;
+    if (b0 >= n) return;
+    uint8_t by[20];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) by[k] = (b0 + k < n) ? in[b0 + k] : 0;
+    uint64_t hi = 0, lo = 0, t2 = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hi = (hi << 8) | by[k];
+#pragma unroll
+    for (int k = 8; k < 16; ++k) lo = (lo << 8) | by[k];
+#pragma unroll
+    for (int k = 16; k < 20; ++k) t2 = (t2 << 8) | by[k];
+    t2 <<= 32;
+    // bits [q, q+64) of the 192-bit window hi:lo:t2 (q < 128)
+    auto get64 = [&](int q) -> uint64_t {
+        if (q == 0) return hi;
+        if (q < 64) return (hi << q) | (lo >> (64 - q));
+        if (q == 64) return lo;
+        return (lo << (q - 64)) | (t2 >> (128 - q));
+    };
+    constexpr uint64_t kBlk = 0x314159265359ull, kEos = 0x177245385090ull;
+    for (int o = 0; o < 64; ++o) {
+        const uint64_t p = b0 * 8 + (uint64_t)o;
+        if (p + 48 > n * 8) break;
+        const uint64_t win = get64(o) >> 16;
+        if (win == kBlk || win == kEos) {
+            const uint32_t nx = (uint32_t)(get64(o + 48) >> 32);  // the 32 bits after the magic
+            const uint32_t slot = atomicAdd(ncand, 1u);
+            if (slot < cap) cand[slot] = DecCand{p, win == kEos ? 1u : 0u, nx};
+        }
+    }
+}
+
+// ---- K2: one wave per candidate block.  `smax` bounds the BWT bytes a block
+// may hold (the largest digit x unit); out + c * stride receives them.
+__global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                      const DecCand* __restrict__ cand, const uint32_t* __restrict__ ids,
+                                                      uint32_t nids, uint32_t smax, uint32_t max_sel,
+                                                      uint8_t* __restrict__ bwt, size_t stride,
+                                                      uint8_t* __restrict__ selbuf, size_t sel_stride,
+                                                      uint32_t* __restrict__ hist_out,
+                                                      DecBlockInfo* __restrict__ infos) {
+    __shared__ HuffLds L;
+    const uint32_t k = blockIdx.x;
+    if (k >= nids) return;
+    const int lane = lane_id();
+    const uint32_t c = uniform(ids[k]);
+    DecBlockInfo* info = infos + k;
+    uint8_t* out = bwt + (size_t)k * stride;
+    (void)selbuf;
+    (void)sel_stride;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L.hist[lane * 4 + j] = 0;
+    BitReader br;
+    br.init(in, n, cand[c].bitpos + 48);
+    if (lane == 0) {
+        info->status = 0;
+        info->end_bit = 0;
+        info->len = 0;
+    }
+    const uint32_t crc = br.bits(16) << 16;
+    const uint32_t crc2 = crc | br.bits(16);
+    const uint32_t rnd = br.bit();
+    const uint32_t orig = br.bits(24);
+    if (lane == 0) {
+        info->crc = crc2;
+        info->orig = orig;
+    }
+    // symbol map (BlockDecompressor.hpp:134-152)
+    const uint32_t used = br.bits(16);
+    uint32_t nsym = 0;
+    for (int i = 0; i < 16; ++i) {
+        if (used & (0x8000u >> i)) {
+            const uint32_t m = br.bits(16);
+            for (int j = 0; j < 16; ++j)
+                if (m & (0x8000u >> j)) {
+                    if (lane == 0) L.symmap[nsym] = (uint8_t)(i * 16 + j);
+                    nsym++;
+                }
+        }
+    }
+    const uint32_t eob = nsym + 1, alpha = nsym + 2;
+    const uint32_t ntab = br.bits(3), nsel = br.bits(15);
+    if (ntab < 2 || ntab > (uint32_t)kMaxTables || nsel < 1 || nsel > max_sel || nsel > (uint32_t)kDecMaxSel) {
+        fail(info, kDecTables);
+        return;
+    }
+    // selectors, MTF-coded in unary (:156-161)
+    {
+        uint32_t mtf = 0x543210u;  // 4-bit entries, front = lowest nibble
+        for (uint32_t i = 0; i < nsel; ++i) {
+            uint32_t u = 0;
+            while (br.bit()) {
+                if (++u >= ntab) break;
+            }
+            if (u >= ntab || br.over) {
+                fail(info, kDecTables);
+                return;
+            }
+            const uint32_t v = (mtf >> (4 * u)) & 15u;
+            const uint32_t below = mtf & ((1u << (4 * u)) - 1u);
+            const uint32_t above = u == 5 ? 0u : (mtf >> (4 * (u + 1))) << (4 * (u + 1));
+            mtf = above | (below << 4) | v;
+            if (lane == 0) {
+                uint32_t& wv = L.sel[i >> 3];
+                wv = (i & 7) ? (wv | (v << (4 * (i & 7)))) : v;
+            }
+        }
+    }
+    // code lengths, delta-coded (:163-174)
+    for (uint32_t t = 0; t < ntab; ++t) {
+        int cur = (int)br.bits(5);
+        for (uint32_t j = 0; j < alpha; ++j) {
+            int guard = 0;
+            while (br.bit()) {
+                cur += br.bit() ? -1 : 1;
+                if (++guard > 40) break;
+            }
+            if (cur < 1 || cur > kMaxDecLen || br.over) {
+                fail(info, kDecTables);
+                return;
+            }
+            if (lane == 0) L.len[t][j] = (uint8_t)cur;
+        }
+    }
+    __syncthreads();
+    // decoding tables (HuffmanStageDecoder.hpp:86-135): lane t < ntab builds
+    // table t's limits, bases and symbol permutation; then all lanes fill the
+    // 9-bit lookup tables
+    if ((uint32_t)lane < ntab) {
+        const int t = lane;
+        uint32_t cnt[kMaxDecLen + 1];
+        for (int l = 0; l <= kMaxDecLen; ++l) cnt[l] = 0;
+        for (uint32_t j = 0; j < alpha; ++j) cnt[L.len[t][j]]++;
+        int32_t code = 0, rank = 0;
+        for (int l = 1; l <= kMaxDecLen; ++l) {
+            if (cnt[l]) {
+                L.base[t][l] = rank - code;
+                L.limit[t][l] = code + (int32_t)cnt[l] - 1;
+            } else {
+                L.base[t][l] = 0;
+                L.limit[t][l] = -1;
+            }
+            rank += (int32_t)cnt[l];
+            code = (code + (int32_t)cnt[l]) << 1;
+        }
+        // permutation: ranks in (length, symbol) order
+        uint32_t next[kMaxDecLen + 1];
+        uint32_t r0 = 0;
+        for (int l = 1; l <= kMaxDecLen; ++l) {
+            next[l] = r0;
+            r0 += cnt[l];
+        }
+        for (uint32_t j = 0; j < alpha; ++j) L.perm[t][next[L.len[t][j]]++] = (uint16_t)j;
+    }
+    for (int i = lane; i < kMaxTables * (1 << kLutBits); i += 64) (&L.lut[0][0])[i] = kLong;
+    __syncthreads();
+    // lookup tables: the symbol of rank R (in (length, symbol) order) has the
+    // code R - base[length]; codes of <= kLutBits bits fill their entries
+    for (uint32_t t = 0; t < ntab; ++t) {
+        for (uint32_t R = lane; R < alpha; R += 64) {
+            const uint32_t j = L.perm[t][R];
+            const uint32_t l = L.len[t][j];
+            if (l > (uint32_t)kLutBits) continue;
+            const uint32_t cj = (uint32_t)((int32_t)R - L.base[t][l]);
+            const uint32_t lo = cj << (kLutBits - l), hi = (cj + 1) << (kLutBits - l);
+            for (uint32_t e = lo; e < hi && e < (1u << kLutBits); ++e) L.lut[t][e] = (uint16_t)(j | (l << 12));
+        }
+    }
+    __syncthreads();
+    if (rnd) {  // BlockDecompressor.hpp:270-273
+        fail(info, kDecRandomised);
+        return;
+    }
+    // ---- data: Huffman symbols -> RUNA/RUNB runs and MTF (HuffmanStageDecoder
+    // ::nextSymbol :48-71, BlockDecompressor::decodeHuffmanData :177-231).
+    // MTF list: entry 4*lane + j in byte j of `ml`.
+    uint32_t ml = (uint32_t)(lane * 4) | (uint32_t)(lane * 4 + 1) << 8 | (uint32_t)(lane * 4 + 2) << 16 |
+                  (uint32_t)(lane * 4 + 3) << 24;
+    // symbol map in registers: symmap[4*lane + j] in byte j
+    uint32_t sm = (uint32_t)L.symmap[lane * 4] | (uint32_t)L.symmap[lane * 4 + 1] << 8 |
+                  (uint32_t)L.symmap[lane * 4 + 2] << 16 | (uint32_t)L.symmap[lane * 4 + 3] << 24;
+    // output staging: 256 bytes per wave, byte q in lane q>>2, byte q&3
+    uint32_t ob = 0;
+    uint32_t oq = 0;  // staged bytes
+    uint32_t olen = 0;     // bytes written before the staging window
+    uint32_t run = 0, inc = 1;
+    uint32_t g = 0, gpos = 0;
+    auto sel_at = [&](uint32_t i) -> uint32_t { return uniform((L.sel[i >> 3] >> (4 * (i & 7))) & 15u); };
+    uint32_t table = sel_at(0);
+    uint32_t status = 0;
+    auto stage_bytes = [&](uint32_t b, uint32_t cnt) {
+        // append cnt copies of byte b
+        while (cnt) {
+            const uint32_t take = min(cnt, 256u - oq);
+            const uint32_t a = lane * 4;  // this lane's first staged byte
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t q = a + j;
+                if (q >= oq && q < oq + take) ob = (ob & ~(0xffu << (8 * j))) | (b << (8 * j));
+            }
+            oq += take;
+            cnt -= take;
+            if (oq == 256) {
+                reinterpret_cast<uint32_t*>(out + olen)[lane] = ob;
+                olen += 256;
+                oq = 0;
+            }
+        }
+    };
+    for (;;) {
+        if (gpos == (uint32_t)kGroupRun) {
+            if (++g >= nsel) {
+                status = kDecData;
+                break;
+            }
+            table = sel_at(g);
+            gpos = 0;
+        }
+        gpos++;
+        const uint32_t e = uniform(L.lut[table][br.peek(kLutBits)]);
+        uint32_t sym, len;
+        if (e != kLong) {
+            sym = e & 0xfffu;
+            len = e >> 12;
+        } else {
+            len = kLutBits + 1;
+            sym = 0xffffffffu;
+            for (; len <= (uint32_t)kMaxDecLen; ++len) {
+                const int32_t cv = (int32_t)br.peek((int)len);
+                if (cv <= L.limit[table][len]) {
+                    sym = L.perm[table][cv + L.base[table][len]];
+                    break;
+                }
+            }
+            if (sym == 0xffffffffu) {
+                status = kDecData;
+                break;
+            }
+        }
+        br.skip((int)len);
+        if (br.over) {
+            status = kDecData;
+            break;
+        }
+        if (sym <= 1) {  // RUNA / RUNB
+            run += inc << sym;
+            inc <<= 1;
+            if (run > smax) {
+                status = kDecSize;
+                break;
+            }
+            continue;
+        }
+        if (run) {
+            if (olen + oq + run > smax) {
+                status = kDecSize;
+                break;
+            }
+            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)ml, 0) & 255u;
+            const uint32_t b = ((uint32_t)__builtin_amdgcn_readlane((int)sm, (int)(f >> 2)) >> (8 * (f & 3))) & 255u;
+            if (lane == 0) atomicAdd(&L.hist[b], run);
+            stage_bytes(b, run);
+            run = 0;
+            inc = 1;
+        }
+        if (sym == eob) break;
+        if (olen + oq >= smax) {
+            status = kDecSize;
+            break;
+        }
+        // move-to-front of index r = sym - 1
+        const uint32_t r = sym - 1, rl = r >> 2, rj = r & 3;
+        const uint32_t v = ((uint32_t)__builtin_amdgcn_readlane((int)ml, (int)rl) >> (8 * rj)) & 255u;
+        const uint32_t up = dpp_mov<dpp::kWaveShr1>(ml);
+        const uint32_t shifted = (ml << 8) | (up >> 24);
+        const uint32_t mask = rj == 3 ? 0xffffffffu : ((1u << (8 * (rj + 1))) - 1u);
+        if ((uint32_t)lane < rl) ml = shifted;
+        else if ((uint32_t)lane == rl) ml = (shifted & mask) | (ml & ~mask);
+        if (lane == 0) ml = (ml & ~0xffu) | v;
+        const uint32_t b = ((uint32_t)__builtin_amdgcn_readlane((int)sm, (int)(v >> 2)) >> (8 * (v & 3))) & 255u;
+        if (lane == 0) atomicAdd(&L.hist[b], 1u);
+        stage_bytes(b, 1);
+    }
+    // flush the staged tail
+    {
+        const uint32_t a = lane * 4;
+        for (int j = 0; j < 4; ++j)
+            if (a + j < oq) out[olen + a + j] = (uint8_t)(ob >> (8 * j));
+    }
+    const uint32_t total = olen + oq;
+    if (status == 0 && orig >= total) status = kDecOrigPtr;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hist_out[(size_t)k * 256 + lane * 4 + j] = L.hist[lane * 4 + j];
+    if (lane == 0) {
+        info->status = status;
+        info->len = total;
+        info->end_bit = br.pos;
+    }
+}
+
+// ---- K3: inverse BWT, one workgroup (256 threads) per block.  merged[r] =
+// (i << 8) | byte for the stable counting sort of the BWT bytes (BlockDecompressor
+// ::initialiseInverseBWT :233-262); the LF cycle from origPtr is the RLE1
+// block.  1024 walkers (4 per thread) start at evenly spaced rows (walker 0 at
+// origPtr), walk to the next start row (pass A: segment lengths and
+// successors), thread 0 chains the segments from walker 0, and the walkers
+// walk again writing their segment's bytes (pass B).
+constexpr int kWalkers = 1024;
+
+__global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict__ bwt, size_t stride,
+                                                       const uint32_t* __restrict__ hist,
+                                                       const DecBlockInfo* __restrict__ infos,
+                                                       const uint32_t* __restrict__ blocks, uint32_t nblocks,
+                                                       uint32_t* __restrict__ merged, size_t mstride,
+                                                       uint32_t* __restrict__ marks, size_t kstride,
+                                                       uint8_t* __restrict__ rle1, size_t rstride,
+                                                       uint32_t* __restrict__ bad_out) {
+    __shared__ uint32_t base[4][256];
+    __shared__ uint32_t seglen[kWalkers];
+    __shared__ uint16_t succ[kWalkers];
+    __shared__ uint32_t segoff[kWalkers];
+    __shared__ uint32_t tmp[8];
+    const uint32_t bi = blockIdx.x;
+    if (bi >= nblocks) return;
+    const uint32_t k = blocks[bi];  // decoded-candidate index
+    const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+    const uint32_t n = infos[k].len;
+    const uint32_t orig = infos[k].orig;
+    const uint8_t* B = bwt + (size_t)k * stride;
+    uint32_t* M = merged + (size_t)bi * mstride;
+    uint32_t* mark = marks + (size_t)bi * kstride;  // walker id of each start row
+    uint8_t* out = rle1 + (size_t)bi * rstride;
+    uint32_t* bad = bad_out + bi;
+    // per-wave counts of each byte over the wave's quarter of the block
+    const uint32_t q0 = (uint32_t)((uint64_t)n * w / 4), q1 = (uint32_t)((uint64_t)n * (w + 1) / 4);
+    for (int j = 0; j < 4; ++j) base[w][lane * 4 + j] = 0;
+    __syncthreads();
+    for (uint32_t p0 = q0; p0 < q1; p0 += 64) {
+        const uint32_t p = p0 + lane;
+        const bool v = p < q1;
+        const uint32_t c = v ? B[p] : 0u;
+        const uint64_t peers = wave_match8(c, v);
+        if (v && (peers & __lanemask_lt()) == 0) atomicAdd(&base[w][c], (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    {
+        // thread t: byte t -> C[t] + counts of the earlier quarters
+        const uint32_t h = hist[(size_t)k * 256 + t];
+        uint32_t total;
+        const uint32_t cb = wg_excl_sum<256>(h, tmp, &total);
+        const uint32_t c0 = base[0][t], c1 = base[1][t], c2 = base[2][t];
+        __syncthreads();
+        base[0][t] = cb;
+        base[1][t] = cb + c0;
+        base[2][t] = cb + c0 + c1;
+        base[3][t] = cb + c0 + c1 + c2;
+    }
+    __syncthreads();
+    for (uint32_t p0 = q0; p0 < q1; p0 += 64) {
+        const uint32_t p = p0 + lane;
+        const bool v = p < q1;
+        const uint32_t c = v ? B[p] : 0u;
+        const uint64_t peers = wave_match8(c, v);
+        const uint64_t below = peers & __lanemask_lt();
+        const uint32_t r = v ? base[w][c] + (uint32_t)__popcll(below) : 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (v && below == 0) base[w][c] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        if (v) M[r] = (p << 8) | c;
+    }
+    // walker starts: walker 0 at origPtr, walker j at j*n/K (skipped when it
+    // collides with an earlier start).  A start row gets bit 31 in merged[]
+    // (i < 2^24, so the bit is free) and its walker id in mark[].
+    __threadfence_block();
+    __syncthreads();
+    auto start_of = [&](int j) -> uint32_t { return j == 0 ? orig : (uint32_t)((uint64_t)n * j / kWalkers); };
+    auto is_start = [&](int j) -> bool {
+        const uint32_t s = start_of(j);
+        return n > 0 && (j == 0 || (s != orig && s != start_of(j - 1)));
+    };
+    for (int j = t; j < kWalkers; j += 256) {
+        segoff[j] = 0xffffffffu;
+        seglen[j] = 0;
+        if (is_start(j)) {
+            const uint32_t s = start_of(j);
+            mark[s] = (uint32_t)j;
+            M[s] |= 0x80000000u;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    // pass A (4 walkers per thread, interleaved): one load per step -- the
+    // entry of the row just reached tells whether it starts a segment
+    uint32_t x[4], len[4], m[4];
+    bool act[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j = t + 256 * q;
+        act[q] = is_start(j);
+        x[q] = start_of(j);
+        len[q] = 0;
+        m[q] = act[q] ? M[x[q]] : 0u;
+    }
+    bool any = true;
+    while (any) {
+        any = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (!act[q]) continue;
+            len[q]++;
+            x[q] = (m[q] & 0x7fffffffu) >> 8;
+            if (x[q] >= n || len[q] > n) {  // inconsistent data: end the walker (never for valid blocks)
+                act[q] = false;
+                if (bad) *bad = 1u;
+                continue;
+            }
+            m[q] = M[x[q]];
+            if (m[q] >> 31) {
+                act[q] = false;
+                seglen[t + 256 * q] = len[q];
+                succ[t + 256 * q] = (uint16_t)mark[x[q]];
+            } else {
+                any = true;
+            }
+        }
+    }
+    __syncthreads();
+    // chain the segments of origPtr's cycle.  A periodic block (T = u^k, the
+    // SURVEY H2 case) has k cycles of n/k rows: the output is the first
+    // cycle's bytes repeated, as the reference's n-step walk produces.
+    __shared__ uint32_t period;
+    if (t == 0) {
+        uint32_t o = 0, j = 0;
+        for (uint32_t guard = 0; guard < (uint32_t)kWalkers && o < n; ++guard) {
+            if (j >= (uint32_t)kWalkers || segoff[j] != 0xffffffffu) break;  // back at walker 0
+            segoff[j] = o;
+            o += seglen[j];
+            j = succ[j];
+        }
+        period = o;
+        if ((o == 0 || o > n || n % o != 0) && bad) *bad = 1u;
+    }
+    __syncthreads();
+    // pass B: write the bytes of each segment
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j = t + 256 * q;
+        act[q] = is_start(j);
+        x[q] = start_of(j);
+        const bool placed = act[q] && segoff[j] != 0xffffffffu && segoff[j] + seglen[j] <= period;
+        len[q] = placed ? seglen[j] : 0u;
+        o[q] = placed ? segoff[j] : 0u;
+    }
+    any = true;
+    while (any) {
+        any = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (!len[q]) continue;
+            const uint32_t mm = M[x[q]] & 0x7fffffffu;
+            out[o[q]++] = (uint8_t)mm;
+            x[q] = mm >> 8;
+            if (x[q] >= n) len[q] = 1;
+            if (--len[q]) any = true;
+        }
+    }
+    const uint32_t per = period;
+    if (per && per < n && n % per == 0) {
+        __threadfence_block();
+        __syncthreads();
+        for (uint32_t i = per + t; i < n; i += 256) out[i] = out[i % per];
+    }
+}
+
+// ---- K4: RLE1 expansion (BlockDecompressor::read :55-88).  States before a
+// byte: 0 = after a count byte or at the block start (any byte: emit 1, ->1),
+// 1..3 = that many equal bytes so far (byte == previous: ->+1, at 3 -> 4 =
+// "next byte is a count"; else emit 1, ->1), 4 = this byte is a count k: emit
+// the run byte k+1 more... the reference emits k+1 copies of the run byte,
+// the fourth included.  pass 0 counts (per chunk and entry state), pass 1
+// writes; chunk c of a block covers [c*n/256, (c+1)*n/256).
+namespace {
+struct Rle1Step {
+    uint32_t st;
+    uint32_t emit;
+};
+__device__ __forceinline__ uint32_t rle1_next(uint32_t st, uint32_t b, uint32_t prev, uint32_t* emit) {
+    if (st == 4) {
+        *emit = b + 1;
+        return 0;
+    }
+    if (st == 0 || b != prev) {
+        *emit = 1;
+        return 1;
+    }
+    if (st == 3) {
+        *emit = 0;
+        return 4;
+    }
+    *emit = 1;
+    return st + 1;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void dec_rle1_kernel(const uint8_t* __restrict__ rle1, size_t rstride,
+                                                       const DecBlockInfo* __restrict__ infos,
+                                                       const uint32_t* __restrict__ blocks, uint32_t nblocks,
+                                                       uint32_t* __restrict__ chunk_state, uint64_t* __restrict__ out_len,
+                                                       const uint64_t* __restrict__ out_off, uint8_t* __restrict__ out,
+                                                       uint64_t cap, uint32_t* __restrict__ crc_out,
+                                                       const uint32_t* __restrict__ crc_table, int pass) {
+    __shared__ uint32_t ctab[256];
+    __shared__ uint32_t clen[256][5];
+    __shared__ uint32_t cexit[256][5];
+    __shared__ uint32_t centry[256];
+    __shared__ uint64_t coff[257];
+    __shared__ uint32_t cpart[256];
+    const uint32_t bi = blockIdx.x;
+    if (bi >= nblocks) return;
+    const int t = threadIdx.x;
+    const uint32_t k = blocks[bi];
+    const uint32_t n = infos[k].len;
+    const uint8_t* X = rle1 + (size_t)bi * rstride;
+    const uint32_t c0 = (uint32_t)((uint64_t)n * t / 256), c1 = (uint32_t)((uint64_t)n * (t + 1) / 256);
+    if (pass == 0) {
+        // all five entry states in lockstep until they agree
+        uint32_t st[5] = {0, 1, 2, 3, 4}, ln[5] = {0, 0, 0, 0, 0};
+        uint32_t p = c0;
+        uint32_t prev = c0 ? X[c0 - 1] : 0xffffffffu;
+        bool same = false;
+        for (; p < c1 && !same; ++p) {
+            const uint32_t b = X[p];
+#pragma unroll
+            for (int s = 0; s < 5; ++s) {
+                uint32_t e;
+                st[s] = rle1_next(st[s], b, prev, &e);
+                ln[s] += e;
+            }
+            prev = b;
+            same = st[0] == st[1] && st[0] == st[2] && st[0] == st[3] && st[0] == st[4];
+        }
+        uint32_t s0 = st[0], tail = 0;
+        for (; p < c1; ++p) {
+            const uint32_t b = X[p];
+            uint32_t e;
+            s0 = rle1_next(s0, b, prev, &e);
+            tail += e;
+            prev = b;
+        }
+        for (int s = 0; s < 5; ++s) {
+            clen[t][s] = ln[s] + tail;
+            cexit[t][s] = same || c0 == c1 ? (c0 == c1 ? (uint32_t)s : s0) : st[s];
+        }
+        __syncthreads();
+        if (t == 0) {
+            uint32_t s = 0;
+            uint64_t o = 0;
+            for (int c = 0; c < 256; ++c) {
+                centry[c] = s;
+                coff[c] = o;
+                o += clen[c][s];
+                s = cexit[c][s];
+            }
+            coff[256] = o;
+        }
+        __syncthreads();
+        chunk_state[(size_t)bi * 256 + t] = centry[t];
+        if (t == 0) out_len[bi] = coff[256];
+        return;
+    }
+    // pass 1: write and CRC
+    ctab[t] = crc_table[t];
+    const uint32_t entry = chunk_state[(size_t)bi * 256 + t];
+    __syncthreads();
+    // chunk output offsets again (entry states known): lengths from one run
+    uint32_t st = entry, prev = c0 ? X[c0 - 1] : 0xffffffffu;
+    uint64_t len = 0;
+    for (uint32_t p = c0; p < c1; ++p) {
+        uint32_t e;
+        const uint32_t b = X[p];
+        st = rle1_next(st, b, prev, &e);
+        len += e;
+        prev = b;
+    }
+    cpart[t] = (uint32_t)len;
+    __syncthreads();
+    if (t == 0) {
+        uint64_t o = 0;
+        for (int c = 0; c < 256; ++c) {
+            coff[c] = o;
+            o += cpart[c];
+        }
+        coff[256] = o;
+    }
+    __syncthreads();
+    const uint64_t base = out_off[bi];
+    uint64_t o = base + coff[t];
+    st = entry;
+    prev = c0 ? X[c0 - 1] : 0xffffffffu;
+    uint32_t runb = c0 >= 1 ? X[c0 - 1] : 0u;  // run byte for a count at the chunk start
+    uint32_t r = 0;                              // CRC register from 0
+    for (uint32_t p = c0; p < c1; ++p) {
+        const uint32_t b = X[p];
+        uint32_t e;
+        const uint32_t was = st;
+        st = rle1_next(st, b, prev, &e);
+        const uint32_t ob = was == 4 ? runb : b;
+        for (uint32_t q = 0; q < e; ++q) {
+            if (o < cap) out[o] = (uint8_t)ob;
+            o++;
+            r = (r << 8) ^ ctab[(r >> 24) ^ ob];
+        }
+        if (was != 4) runb = b;
+        prev = b;
+    }
+    // block CRC: chunk registers shifted by the bytes after them
+    const uint64_t after = coff[256] - coff[t + 1];
+    cpart[t] = crc_shift(r, after);
+    __syncthreads();
+    if (t < 64) {
+        uint32_t v = cpart[t] ^ cpart[t + 64] ^ cpart[t + 128] ^ cpart[t + 192];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d);
+        if (t == 0) crc_out[bi] = ~(v ^ crc_shift(0xffffffffu, coff[256]));
+    }
+}
+
+int dec_set_xpow8(const uint32_t* tab64) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_xpow8), tab64, 64 * sizeof(uint32_t)) == hipSuccess ? 0 : -1;
+}
+
+}  // namespace bz2mi

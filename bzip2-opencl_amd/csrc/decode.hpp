@@ -1,0 +1,48 @@
+// Device bzip2 decoder (decode.hip): shared types and kernel entry points.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bz2mi {
+
+// a 48-bit magic found in the stream: bit position, 0 = block header /
+// 1 = end of stream, and the 32 bits that follow it (the stored CRC)
+struct DecCand {
+    uint64_t bitpos;
+    uint32_t type;
+    uint32_t next32;
+};
+
+// status codes of a decoded block (messages in dapi: the reference's texts)
+enum : uint32_t {
+    kDecOk = 0,
+    kDecTables = 1,      // "block Huffman tables invalid"       BlockDecompressor.hpp:158-162
+    kDecData = 2,        // "Error decoding  block"              HuffmanStageDecoder.hpp:55,70
+    kDecSize = 3,        // "BZip2 block exceeds declared block size"  BlockDecompressor.hpp:211,226
+    kDecOrigPtr = 4,     // "BZip2 start pointer invalid"         BlockDecompressor.hpp:237
+    kDecRandomised = 5,  // "BZip2 randomised blocks not implemented"  BlockDecompressor.hpp:272
+};
+
+struct DecBlockInfo {
+    uint64_t end_bit;  // first bit after the block (after its end-of-block symbol)
+    uint32_t status;
+    uint32_t orig;     // origPtr
+    uint32_t len;      // BWT (= RLE1) bytes
+    uint32_t crc;      // stored block CRC
+};
+
+__global__ void dec_scan_kernel(const uint8_t* in, uint64_t n, DecCand* cand, uint32_t* ncand, uint32_t cap);
+__global__ void dec_huff_kernel(const uint8_t* in, uint64_t n, const DecCand* cand, const uint32_t* ids,
+                                uint32_t nids, uint32_t smax, uint32_t max_sel, uint8_t* bwt, size_t stride,
+                                uint8_t* selbuf, size_t sel_stride, uint32_t* hist_out, DecBlockInfo* infos);
+__global__ void dec_ibwt_kernel(const uint8_t* bwt, size_t stride, const uint32_t* hist, const DecBlockInfo* infos,
+                                const uint32_t* blocks, uint32_t nblocks, uint32_t* merged, size_t mstride,
+                                uint32_t* marks, size_t kstride, uint8_t* rle1, size_t rstride, uint32_t* bad);
+__global__ void dec_rle1_kernel(const uint8_t* rle1, size_t rstride, const DecBlockInfo* infos,
+                                const uint32_t* blocks, uint32_t nblocks, uint32_t* chunk_state, uint64_t* out_len,
+                                const uint64_t* out_off, uint8_t* out, uint64_t cap, uint32_t* crc_out,
+                                const uint32_t* crc_table, int pass);
+int dec_set_xpow8(const uint32_t* tab64);
+
+}  // namespace bz2mi

@@ -28,6 +28,8 @@ extern "C" {
 #define BZ2MI_EDEVICE -2   /* HIP runtime failure (reference: print_error + exit(1)) */
 #define BZ2MI_ESPACE -3    /* output buffer too small */
 #define BZ2MI_ESTATE -4    /* call out of order (e.g. write after finish) */
+#define BZ2MI_EFORMAT -5   /* corrupt or unsupported .bz2 data (reference: std::runtime_error
+                              from InputStream / BlockDecompressor; the message is the reference's) */
 
 typedef struct bz2mi_ctx bz2mi_ctx;
 
@@ -116,6 +118,37 @@ int bz2mi_last_stats(bz2mi_ctx* ctx, uint64_t* out8);
 
 /* Number of blocks compressed so far in this stream. */
 uint64_t bz2mi_blocks_done(const bz2mi_ctx* ctx);
+
+/* ---- decompression on the device ----------
+ * Replaces the reference's InputStream (InputStream.hpp:36-159),
+ * BlockDecompressor (BlockDecompressor.hpp:37-282) and HuffmanStageDecoder
+ * (HuffmanStageDecoder.hpp:30-136): every block of the stream is decoded at
+ * once.  Errors are BZ2MI_EFORMAT with the reference's message ("Invalid BZip2
+ * header", "BZip2 block CRC error", "BZip2 stream CRC error", "BZip2 stream
+ * format error", "block Huffman tables invalid", "Error decoding  block",
+ * "BZip2 block exceeds declared block size", "BZip2 start pointer invalid",
+ * "BZip2 randomised blocks not implemented"), reported for the first failing
+ * block in stream order as the reference's byte-at-a-time decoder would.
+ *   unit   block-size unit of the digit in "BZh<digit>": 10000 = the
+ *          reference's limit (Config.hpp:30), 100000 = stock bzip2 files.
+ * Concatenated streams are decoded one after another (bzip2's behaviour; the
+ * reference stops after the first).  Bytes after the last stream that do not
+ * start a new "BZh" header are ignored.
+ */
+typedef struct bz2mi_dctx bz2mi_dctx;
+bz2mi_dctx* bz2mi_dcreate(int unit, int device);
+void bz2mi_ddestroy(bz2mi_dctx* d);
+
+/* host buffers; on BZ2MI_ESPACE *out_len receives the size needed */
+int bz2mi_decompress(bz2mi_dctx* d, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
+
+/* device buffers (HBM); hip_stream: hipStream_t or NULL (the context's) */
+int bz2mi_decompress_device(bz2mi_dctx* d, const void* d_in, size_t n, void* d_out, size_t cap, size_t* out_len,
+                            void* hip_stream);
+
+/* milliseconds of the last call: [0] candidate scan, [1] Huffman + MTF + RLE2,
+ * [2] inverse BWT, [3] RLE1 + CRC, [4] whole call */
+int bz2mi_dlast_timings(bz2mi_dctx* d, float* ms5);
 
 #ifdef __cplusplus
 }
