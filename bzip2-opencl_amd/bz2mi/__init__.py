@@ -281,9 +281,9 @@ class Decompressor:
         return out_len.value
 
     def timings(self):
-        arr = (ctypes.c_float * 5)()
+        arr = (ctypes.c_float * 6)()
         _check(lib().bz2mi_dlast_timings(self._h, arr))
-        return dict(zip(("scan", "huffman", "ibwt", "rle1", "total"), list(arr)))
+        return dict(zip(("scan", "huffman", "mtf", "ibwt", "rle1", "total"), list(arr)))
 
 
 def decompress(data, unit: int = 10000, device: int = 0) -> bytes:

@@ -62,10 +62,10 @@ struct bz2mi_dctx {
     size_t ids_cap = 0;
     uint8_t* d_bwt = nullptr;
     size_t bwt_cap = 0;
-    uint8_t* d_sel = nullptr;
-    size_t sel_cap = 0;
-    uint32_t* d_hist = nullptr;
-    size_t hist_cap = 0;
+    uint16_t* d_syms = nullptr;
+    size_t syms_cap = 0;
+    uint8_t* d_symmap = nullptr;
+    size_t symmap_cap = 0;
     bz2mi::DecBlockInfo* d_info = nullptr;
     size_t info_cap = 0;
     uint32_t* d_blocks = nullptr;
@@ -90,8 +90,8 @@ struct bz2mi_dctx {
     size_t in_cap = 0;
     uint8_t* d_out = nullptr;  // staging for host output
     size_t out_cap = 0;
-    hipEvent_t ev[5] = {};
-    float ms[5] = {0, 0, 0, 0, 0};
+    hipEvent_t ev[6] = {};
+    float ms[6] = {0, 0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -135,18 +135,16 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
     const uint32_t smax = (uint32_t)(9 * d->unit);
     const uint32_t max_sel = d->unit == 10000 ? (uint32_t)(smax / 50 + 1) : (uint32_t)(smax / 50 + 2);
     const size_t stride = ((size_t)smax + 255) & ~(size_t)255;
-    const size_t sel_stride = ((size_t)max_sel + 63) & ~(size_t)63;
+    const size_t sym_stride = ((size_t)smax + 2 + 63) & ~(size_t)63;
     const size_t nk = ids.size();
     if ((r = grow(&d->d_ids, &d->ids_cap, nk))) return r;
-    if ((r = grow(&d->d_bwt, &d->bwt_cap, nk * stride))) return r;
-    if ((r = grow(&d->d_sel, &d->sel_cap, nk * sel_stride))) return r;
-    if ((r = grow(&d->d_hist, &d->hist_cap, nk * 256))) return r;
+    if ((r = grow(&d->d_syms, &d->syms_cap, nk * sym_stride))) return r;
+    if ((r = grow(&d->d_symmap, &d->symmap_cap, nk * 256))) return r;
     if ((r = grow(&d->d_info, &d->info_cap, nk))) return r;
     if (nk) {
         DCHECK(hipMemcpyAsync(d->d_ids, ids.data(), nk * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(dec_huff_kernel, dim3((unsigned)nk), dim3(64), 0, s, d_in, (uint64_t)n, d->d_cand,
-                           d->d_ids, (uint32_t)nk, smax, max_sel, d->d_bwt, stride, d->d_sel, sel_stride, d->d_hist,
-                           d->d_info);
+        hipLaunchKernelGGL(dec_huff_kernel, dim3((unsigned)nk), dim3(64), (max_sel + 7) / 8 * 4, s, d_in, (uint64_t)n, d->d_cand,
+                           d->d_ids, (uint32_t)nk, smax, max_sel, d->d_syms, sym_stride, d->d_symmap, d->d_info);
         DCHECK(hipGetLastError());
     }
     std::vector<DecBlockInfo> info(nk);
@@ -157,9 +155,9 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
         if (FILE* f = fopen(dump, "wb")) {
             if (nk) {
                 fwrite(&info[0], sizeof(DecBlockInfo), 1, f);
-                std::vector<uint8_t> b(std::min<size_t>(info[0].len, stride));
-                DCHECK(hipMemcpy(b.data(), d->d_bwt, b.size(), hipMemcpyDeviceToHost));
-                fwrite(b.data(), 1, b.size(), f);
+                std::vector<uint16_t> b(std::min<size_t>(info[0].nsym, sym_stride));
+                DCHECK(hipMemcpy(b.data(), d->d_syms, b.size() * 2, hipMemcpyDeviceToHost));
+                fwrite(b.data(), 2, b.size(), f);
             }
             fclose(f);
         }
@@ -180,6 +178,7 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
     };
     std::vector<uint32_t> chain;       // decoded-candidate ids, stream order
     std::vector<uint32_t> chain_crc;   // stored block CRCs
+    std::vector<uint32_t> chain_S;     // the block size limit of each block's stream
     std::vector<uint32_t> stream_end;  // chain index where each stream ends
     std::vector<uint32_t> stream_crc;  // stored stream CRCs
     int err_status = -1;               // first structural / decode error after the chain
@@ -223,11 +222,6 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
                 err_msg = dec_message(info[k].status);
                 break;
             }
-            if (info[k].len > S) {
-                err_status = kDecSize;
-                err_msg = dec_message(kDecSize);
-                break;
-            }
             if (info[k].end_bit > (uint64_t)n * 8) {
                 err_status = 0;
                 err_msg = "Insufficient data";
@@ -235,18 +229,50 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
             }
             chain.push_back(k);
             chain_crc.push_back(info[k].crc);
+            chain_S.push_back(S);
             pos = info[k].end_bit;
         }
         if (!ended) break;
         byte = (pos + 7) / 8;
     }
+    // ---- K2b (MTF / RLE2) over the blocks of the chain; its errors (block
+    // size, origPtr) end the chain at the first failing block
+    if (!chain.empty()) {
+        if ((r = grow(&d->d_blocks, &d->blocks_cap, chain.size()))) return r;
+        if ((r = grow(&d->d_bwt, &d->bwt_cap, nk * stride))) return r;
+        // d_merged (the inverse BWT's vector, free until then) is the scratch
+        if ((r = grow(&d->d_merged, &d->merged_cap, chain.size() * sym_stride))) return r;
+        DCHECK(hipMemcpyAsync(d->d_blocks, chain.data(), chain.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(dec_mtf_kernel, dim3((unsigned)chain.size()), dim3(64), 0, s, d->d_syms, sym_stride,
+                           d->d_symmap, d->d_blocks, (uint32_t)chain.size(), smax, d->d_merged, sym_stride,
+                           d->d_bwt, stride, d->d_info);
+        DCHECK(hipGetLastError());
+        DCHECK(hipMemcpyAsync(info.data(), d->d_info, nk * sizeof(DecBlockInfo), hipMemcpyDeviceToHost, s));
+        DCHECK(hipStreamSynchronize(s));
+        for (size_t i = 0; i < chain.size(); ++i) {
+            const DecBlockInfo& bi = info[chain[i]];
+            const uint32_t st = bi.status ? bi.status : (bi.len > chain_S[i] ? (uint32_t)kDecSize : 0u);
+            if (st) {
+                err_status = (int)st;
+                err_msg = dec_message(st);
+                chain.resize(i);
+                chain_crc.resize(i);
+                while (!stream_end.empty() && stream_end.back() > i) {
+                    stream_end.pop_back();
+                    stream_crc.pop_back();
+                }
+                break;
+            }
+        }
+    }
+    DCHECK(hipEventRecord(d->ev[3], s));
     // ---- K3 / K4 over the blocks of the chain
     const size_t nb = chain.size();
     std::vector<uint64_t> olen(nb), ooff(nb + 1, 0);
     std::vector<uint32_t> crc(nb), bad(nb, 0);
     if (nb) {
         if ((r = grow(&d->d_blocks, &d->blocks_cap, nb))) return r;
-        if ((r = grow(&d->d_merged, &d->merged_cap, nb * stride))) return r;
+        if ((r = grow(&d->d_merged, &d->merged_cap, std::max(nb * stride, nb * sym_stride)))) return r;
         if ((r = grow(&d->d_marks, &d->marks_cap, nb * stride))) return r;
         if ((r = grow(&d->d_rle1, &d->rle1_cap, nb * stride))) return r;
         if ((r = grow(&d->d_cstate, &d->cstate_cap, nb * 256))) return r;
@@ -256,11 +282,10 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
         if ((r = grow(&d->d_bad, &d->bad_cap, nb))) return r;
         DCHECK(hipMemsetAsync(d->d_bad, 0, nb * sizeof(uint32_t), s));
         DCHECK(hipMemcpyAsync(d->d_blocks, chain.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(dec_ibwt_kernel, dim3((unsigned)nb), dim3(256), 0, s, d->d_bwt, stride, d->d_hist,
-                           d->d_info, d->d_blocks, (uint32_t)nb, d->d_merged, stride, d->d_marks, stride, d->d_rle1,
+        hipLaunchKernelGGL(dec_ibwt_kernel, dim3((unsigned)nb), dim3(256), 0, s, d->d_bwt, stride, d->d_info, d->d_blocks, (uint32_t)nb, d->d_merged, stride, d->d_marks, stride, d->d_rle1,
                            stride, d->d_bad);
         DCHECK(hipGetLastError());
-        DCHECK(hipEventRecord(d->ev[3], s));
+        DCHECK(hipEventRecord(d->ev[4], s));
         hipLaunchKernelGGL(dec_rle1_kernel, dim3((unsigned)nb), dim3(256), 0, s, d->d_rle1, stride, d->d_info,
                            d->d_blocks, (uint32_t)nb, d->d_cstate, d->d_olen, (const uint64_t*)nullptr,
                            (uint8_t*)nullptr, (uint64_t)0, d->d_crc, d->d_crctab, 0);
@@ -280,9 +305,9 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
         DCHECK(hipMemcpyAsync(crc.data(), d->d_crc, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         DCHECK(hipMemcpyAsync(bad.data(), d->d_bad, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     } else {
-        DCHECK(hipEventRecord(d->ev[3], s));
+        DCHECK(hipEventRecord(d->ev[4], s));
     }
-    DCHECK(hipEventRecord(d->ev[4], s));
+    DCHECK(hipEventRecord(d->ev[5], s));
     DCHECK(hipStreamSynchronize(s));
     // ---- checks in stream order: block CRCs (BlockDecompressor::checkCRC
     // :101-109), stream CRCs (InputStream.hpp:136-143), then the first error
@@ -309,8 +334,8 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
     if (err_status >= 0) return bz2mi_set_error(BZ2MI_EFORMAT, err_msg);
     *out_len = nb ? ooff[nb] : 0;
     float t;
-    for (int k = 0; k < 4; ++k) d->ms[k] = hipEventElapsedTime(&t, d->ev[k], d->ev[k + 1]) == hipSuccess ? t : 0.f;
-    d->ms[4] = hipEventElapsedTime(&t, d->ev[0], d->ev[4]) == hipSuccess ? t : 0.f;
+    for (int k = 0; k < 5; ++k) d->ms[k] = hipEventElapsedTime(&t, d->ev[k], d->ev[k + 1]) == hipSuccess ? t : 0.f;
+    d->ms[5] = hipEventElapsedTime(&t, d->ev[0], d->ev[5]) == hipSuccess ? t : 0.f;
     return BZ2MI_OK;
 }
 
@@ -369,7 +394,7 @@ void bz2mi_ddestroy(bz2mi_dctx* d) {
     (void)hipSetDevice(d->device);
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     for (void* p : {(void*)d->d_crctab, (void*)d->d_cnt, (void*)d->d_cand, (void*)d->d_ids, (void*)d->d_bwt,
-                    (void*)d->d_sel, (void*)d->d_hist, (void*)d->d_info, (void*)d->d_blocks, (void*)d->d_merged,
+                    (void*)d->d_syms, (void*)d->d_symmap, (void*)d->d_info, (void*)d->d_blocks, (void*)d->d_merged,
                     (void*)d->d_marks, (void*)d->d_rle1, (void*)d->d_cstate, (void*)d->d_olen, (void*)d->d_ooff,
                     (void*)d->d_crc, (void*)d->d_in, (void*)d->d_out})
         if (p) (void)hipFree(p);
@@ -407,9 +432,9 @@ int bz2mi_decompress(bz2mi_dctx* d, const uint8_t* in, size_t n, uint8_t* out, s
     return BZ2MI_OK;
 }
 
-int bz2mi_dlast_timings(bz2mi_dctx* d, float* ms5) {
-    if (!d || !ms5) return bz2mi_set_error(BZ2MI_EINVAL, "null argument");
-    for (int k = 0; k < 5; ++k) ms5[k] = d->ms[k];
+int bz2mi_dlast_timings(bz2mi_dctx* d, float* ms6) {
+    if (!d || !ms6) return bz2mi_set_error(BZ2MI_EINVAL, "null argument");
+    for (int k = 0; k < 6; ++k) ms6[k] = d->ms[k];
     return BZ2MI_OK;
 }
 

@@ -65,7 +65,10 @@ struct BitReader {
     uint64_t pos;       // next bit (absolute)
     uint64_t buf;       // MSB-aligned pending bits
     int nb;             // valid bits in buf
-    uint64_t wnext;     // next word to load
+    uint64_t res;       // next 64 bits (reserve), MSB first
+    int rb;             // valid bits in res (0, 32 or 64)
+    uint64_t pf;        // the 64 bits after res, loaded ahead (prefetch)
+    uint64_t wnext;     // word index of the next prefetch
     bool over;          // read past the end
 
     __device__ __forceinline__ uint32_t word(uint64_t i) const {
@@ -77,39 +80,55 @@ struct BitReader {
         for (int q = 0; q < 4; ++q) x = (x << 8) | ((i * 4 + q < nbytes) ? b[i * 4 + q] : 0u);
         return x;
     }
+    __device__ __forceinline__ uint64_t load64(uint64_t i) const {
+        return ((uint64_t)word(i) << 32) | word(i + 1);
+    }
     __device__ void init(const uint8_t* base, uint64_t nbytes, uint64_t bitpos) {
-        // `base` is 4-byte aligned; the tail word may be partial (masked by nbits)
+        // `base` is 4-byte aligned
         w = reinterpret_cast<const uint32_t*>(base);
         nbits = nbytes * 8;
         pos = bitpos;
-        wnext = bitpos >> 5;
+        const uint64_t w0 = bitpos >> 5;
         const int off = (int)(bitpos & 31);
-        buf = 0;
-        nb = 0;
+        buf = load64(w0) << off;
+        nb = 64 - off;
+        res = load64(w0 + 2);
+        rb = 64;
+        pf = load64(w0 + 4);
+        wnext = w0 + 6;
         over = false;
-        refill();
-        buf <<= off;
-        nb -= off;
     }
+    // keep > 32 bits in buf: 32 bits move from the reserve; an empty reserve
+    // takes the prefetched 64 bits and the next prefetch is issued (its
+    // latency is covered by the ~64 bits decoded meanwhile)
     __device__ __forceinline__ void refill() {
-        while (nb <= 32) {
-            const uint32_t x = word(wnext);
-            buf |= (uint64_t)x << (32 - nb);
+        if (nb <= 32) {
+            buf |= (res >> 32) << (32 - nb);
+            res <<= 32;
+            rb -= 32;
             nb += 32;
-            wnext++;
+            if (rb == 0) {
+                res = pf;
+                rb = 64;
+                pf = load64(wnext);
+                wnext += 2;
+            }
         }
     }
     __device__ __forceinline__ uint32_t peek(int k) const { return (uint32_t)(buf >> (64 - k)); }
-    __device__ __forceinline__ void skip(int k) {
+    __device__ __forceinline__ void skip(int k) {  // k <= 32
         buf <<= k;
         nb -= k;
         pos += k;
+        refill();
+    }
+    __device__ __forceinline__ void check() {
         if (pos > nbits) over = true;
-        if (nb <= 32) refill();
     }
     __device__ __forceinline__ uint32_t bits(int k) {  // 1..32
         const uint32_t v = peek(k);
         skip(k);
+        check();
         return v;
     }
     __device__ __forceinline__ uint32_t bit() { return bits(1); }
@@ -126,9 +145,7 @@ struct HuffLds {
     int32_t base[kMaxTables][kMaxDecLen + 2];  // rank of the first code of a length minus that code
     uint16_t perm[kMaxTables][kMaxAlpha];       // symbols by (length, symbol)
     uint8_t len[kMaxTables][kMaxAlpha];
-    uint32_t hist[256];
     uint8_t symmap[256];
-    uint32_t sel[(kDecMaxSel + 7) / 8];  // selectors, 4 bits each
 };
 
 __device__ __forceinline__ void fail(DecBlockInfo* info, uint32_t code) {
@@ -176,32 +193,29 @@ __global__ __launch_bounds__(256) void dec_scan_kernel(const uint8_t* __restrict
     }
 }
 
-// ---- K2: one wave per candidate block.  `smax` bounds the BWT bytes a block
-// may hold (the largest digit x unit); out + c * stride receives them.
+// ---- K2: one wave per candidate block: header, symbol map, selectors, code
+// lengths, decoding tables, then the Huffman symbols.  `smax` bounds the BWT
+// bytes a block may hold (the largest digit x unit).
 __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict__ in, uint64_t n,
                                                       const DecCand* __restrict__ cand, const uint32_t* __restrict__ ids,
                                                       uint32_t nids, uint32_t smax, uint32_t max_sel,
-                                                      uint8_t* __restrict__ bwt, size_t stride,
-                                                      uint8_t* __restrict__ selbuf, size_t sel_stride,
-                                                      uint32_t* __restrict__ hist_out,
+                                                      uint16_t* __restrict__ syms, size_t sym_stride,
+                                                      uint8_t* __restrict__ symmap_out,
                                                       DecBlockInfo* __restrict__ infos) {
     __shared__ HuffLds L;
+    extern __shared__ uint32_t sel_lds[];  // selectors, 4 bits each ((max_sel + 7) / 8 words)
     const uint32_t k = blockIdx.x;
     if (k >= nids) return;
     const int lane = lane_id();
     const uint32_t c = uniform(ids[k]);
     DecBlockInfo* info = infos + k;
-    uint8_t* out = bwt + (size_t)k * stride;
-    (void)selbuf;
-    (void)sel_stride;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) L.hist[lane * 4 + j] = 0;
     BitReader br;
     br.init(in, n, cand[c].bitpos + 48);
     if (lane == 0) {
         info->status = 0;
         info->end_bit = 0;
         info->len = 0;
+        info->nsym = 0;
     }
     const uint32_t crc = br.bits(16) << 16;
     const uint32_t crc2 = crc | br.bits(16);
@@ -247,7 +261,7 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
             const uint32_t above = u == 5 ? 0u : (mtf >> (4 * (u + 1))) << (4 * (u + 1));
             mtf = above | (below << 4) | v;
             if (lane == 0) {
-                uint32_t& wv = L.sel[i >> 3];
+                uint32_t& wv = sel_lds[i >> 3];
                 wv = (i & 7) ? (wv | (v << (4 * (i & 7)))) : v;
             }
         }
@@ -317,42 +331,18 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
         fail(info, kDecRandomised);
         return;
     }
-    // ---- data: Huffman symbols -> RUNA/RUNB runs and MTF (HuffmanStageDecoder
-    // ::nextSymbol :48-71, BlockDecompressor::decodeHuffmanData :177-231).
-    // MTF list: entry 4*lane + j in byte j of `ml`.
-    uint32_t ml = (uint32_t)(lane * 4) | (uint32_t)(lane * 4 + 1) << 8 | (uint32_t)(lane * 4 + 2) << 16 |
-                  (uint32_t)(lane * 4 + 3) << 24;
-    // symbol map in registers: symmap[4*lane + j] in byte j
-    uint32_t sm = (uint32_t)L.symmap[lane * 4] | (uint32_t)L.symmap[lane * 4 + 1] << 8 |
-                  (uint32_t)L.symmap[lane * 4 + 2] << 16 | (uint32_t)L.symmap[lane * 4 + 3] << 24;
-    // output staging: 256 bytes per wave, byte q in lane q>>2, byte q&3
-    uint32_t ob = 0;
-    uint32_t oq = 0;  // staged bytes
-    uint32_t olen = 0;     // bytes written before the staging window
-    uint32_t run = 0, inc = 1;
+    // ---- data, part 1: the Huffman symbols (HuffmanStageDecoder::nextSymbol
+    // :48-71), the only serial chain of the block: one LDS lookup and a few
+    // scalar operations per symbol.  Symbols are gathered 64 at a time in a
+    // VGPR (v_writelane) and stored coalesced; MTF / RLE2 are dec_mtf_kernel's.
     uint32_t g = 0, gpos = 0;
-    auto sel_at = [&](uint32_t i) -> uint32_t { return uniform((L.sel[i >> 3] >> (4 * (i & 7))) & 15u); };
+    auto sel_at = [&](uint32_t i) -> uint32_t { return uniform((sel_lds[i >> 3] >> (4 * (i & 7))) & 15u); };
     uint32_t table = sel_at(0);
     uint32_t status = 0;
-    auto stage_bytes = [&](uint32_t b, uint32_t cnt) {
-        // append cnt copies of byte b
-        while (cnt) {
-            const uint32_t take = min(cnt, 256u - oq);
-            const uint32_t a = lane * 4;  // this lane's first staged byte
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t q = a + j;
-                if (q >= oq && q < oq + take) ob = (ob & ~(0xffu << (8 * j))) | (b << (8 * j));
-            }
-            oq += take;
-            cnt -= take;
-            if (oq == 256) {
-                reinterpret_cast<uint32_t*>(out + olen)[lane] = ob;
-                olen += 256;
-                oq = 0;
-            }
-        }
-    };
+    uint32_t ns = 0;       // symbols decoded
+    uint32_t chunk = 0;    // symbol ns & 63 of the current chunk in lane ns & 63
+    uint16_t* so = syms + (size_t)k * sym_stride;
+    const uint32_t ns_max = smax + 2;
     for (;;) {
         if (gpos == (uint32_t)kGroupRun) {
             if (++g >= nsel) {
@@ -384,64 +374,227 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
             }
         }
         br.skip((int)len);
-        if (br.over) {
+        if (br.pos > br.nbits) {
             status = kDecData;
             break;
         }
-        if (sym <= 1) {  // RUNA / RUNB
-            run += inc << sym;
-            inc <<= 1;
-            if (run > smax) {
-                status = kDecSize;
-                break;
-            }
-            continue;
-        }
-        if (run) {
-            if (olen + oq + run > smax) {
-                status = kDecSize;
-                break;
-            }
-            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)ml, 0) & 255u;
-            const uint32_t b = ((uint32_t)__builtin_amdgcn_readlane((int)sm, (int)(f >> 2)) >> (8 * (f & 3))) & 255u;
-            if (lane == 0) atomicAdd(&L.hist[b], run);
-            stage_bytes(b, run);
-            run = 0;
-            inc = 1;
-        }
+        chunk = (uint32_t)lane == (ns & 63u) ? sym : chunk;
+        ns++;
+        if ((ns & 63u) == 0) so[ns - 64 + lane] = (uint16_t)chunk;
         if (sym == eob) break;
-        if (olen + oq >= smax) {
+        if (ns >= ns_max) {
             status = kDecSize;
             break;
         }
-        // move-to-front of index r = sym - 1
-        const uint32_t r = sym - 1, rl = r >> 2, rj = r & 3;
-        const uint32_t v = ((uint32_t)__builtin_amdgcn_readlane((int)ml, (int)rl) >> (8 * rj)) & 255u;
-        const uint32_t up = dpp_mov<dpp::kWaveShr1>(ml);
-        const uint32_t shifted = (ml << 8) | (up >> 24);
-        const uint32_t mask = rj == 3 ? 0xffffffffu : ((1u << (8 * (rj + 1))) - 1u);
-        if ((uint32_t)lane < rl) ml = shifted;
-        else if ((uint32_t)lane == rl) ml = (shifted & mask) | (ml & ~mask);
-        if (lane == 0) ml = (ml & ~0xffu) | v;
-        const uint32_t b = ((uint32_t)__builtin_amdgcn_readlane((int)sm, (int)(v >> 2)) >> (8 * (v & 3))) & 255u;
-        if (lane == 0) atomicAdd(&L.hist[b], 1u);
-        stage_bytes(b, 1);
     }
-    // flush the staged tail
-    {
-        const uint32_t a = lane * 4;
-        for (int j = 0; j < 4; ++j)
-            if (a + j < oq) out[olen + a + j] = (uint8_t)(ob >> (8 * j));
-    }
-    const uint32_t total = olen + oq;
-    if (status == 0 && orig >= total) status = kDecOrigPtr;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) hist_out[(size_t)k * 256 + lane * 4 + j] = L.hist[lane * 4 + j];
+    if ((ns & 63u) && (uint32_t)lane < (ns & 63u)) so[(ns & ~63u) + lane] = (uint16_t)chunk;
     if (lane == 0) {
         info->status = status;
-        info->len = total;
+        info->nsym = ns;
+        info->alpha = nsym;
         info->end_bit = br.pos;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) symmap_out[(size_t)k * 256 + lane * 4 + j] = L.symmap[lane * 4 + j];
+}
+
+// ---- K2b: data, part 2 (BlockDecompressor::decodeHuffmanData :177-231):
+// RUNA/RUNB runs and inverse move-to-front, one wave per block of the chain.
+// Lane c takes the c-th 64th of the block's symbols (its start moved past run
+// digits, so no run is split), and the serial list is broken up:
+//   pass A  every lane decodes its chunk against a *symbolic* start list
+//           (entries = indices into the list at its chunk start): its own
+//           recency list (LDS, 4 entries per word, [word][lane]) and the set
+//           of start indices it took (LDS bit set).  Rank r < D picks recency
+//           entry r; r >= D picks the (r-D)-th untaken start index.  Every
+//           symbol leaves (symbolic value | byte count << 8) in a scratch word;
+//   pass B  the start lists are composed left to right (entries = output
+//           bytes, list 0 = the symbol map):
+//           list_{c+1} = list_c[recency_c] ++ list_c[untaken_c ascending],
+//   pass C  and, with list_c known, the wave writes chunk c's bytes (lanes on
+//           consecutive symbols, offsets by a wave scan of the byte counts).
+// A symbol costs its lane ~rank/4 LDS word shifts instead of a serial pass
+// of the whole wave.
+struct MtfLds {
+    uint32_t rec[64][64];    // [word][lane] recency list, entry 4w+j in byte j
+    uint32_t used[8][64];    // [word][lane] start indices taken
+    uint8_t lists[2][256];   // start lists of chunk c and c+1, as output bytes
+};
+
+__device__ __forceinline__ uint32_t select_zero(uint32_t u, uint32_t k) {
+    // index of the k-th (0-based) zero bit of u, LSB first (k < popc(~u))
+    uint32_t x = ~u, pos = 0;
+#pragma unroll
+    for (int sh = 16; sh; sh >>= 1) {
+        const uint32_t c = (uint32_t)__popc(x & ((1u << sh) - 1u));
+        if (k >= c) {
+            k -= c;
+            x >>= sh;
+            pos += sh;
+        }
+    }
+    return pos;
+}
+
+__global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict__ syms, size_t sym_stride,
+                                                     const uint8_t* __restrict__ symmaps,
+                                                     const uint32_t* __restrict__ blocks, uint32_t nblocks,
+                                                     uint32_t smax, uint32_t* __restrict__ scratch, size_t sstride,
+                                                     uint8_t* __restrict__ bwt, size_t stride,
+                                                     DecBlockInfo* __restrict__ infos) {
+    __shared__ MtfLds L;
+    const uint32_t bi = blockIdx.x;
+    if (bi >= nblocks) return;
+    const int lane = lane_id();
+    const uint32_t k = uniform(blocks[bi]);
+    DecBlockInfo* info = infos + k;
+    const uint32_t ns = uniform(info->nsym), eob = uniform(info->alpha) + 1, orig = uniform(info->orig);
+    const uint16_t* so = syms + (size_t)k * sym_stride;
+    uint32_t* tv = scratch + (size_t)bi * sstride;
+    uint8_t* out = bwt + (size_t)k * stride;
+    // chunk [a, b): nominal 64th, start moved past run digits
+    uint32_t a = (uint32_t)((uint64_t)ns * (uint32_t)lane / 64u);
+    if (lane)
+        while (a < ns && so[a] <= 1) ++a;
+    const uint32_t an = (uint32_t)__shfl_down((int)a, 1);
+    const uint32_t b = lane == 63 ? ns : an;
+    // ---- pass A
+#pragma unroll
+    for (int w = 0; w < 8; ++w) L.used[w][lane] = 0;
+    uint32_t D = 0, run = 0, inc = 1, runpos = 0, cnt = 0;
+    bool inrun = false;
+    auto flush_run = [&]() {
+        const uint32_t front = D ? (L.rec[0][lane] & 255u) : 0u;
+        tv[runpos] = front | (run << 8);
+        cnt += run;
+        inrun = false;
+    };
+    for (uint32_t p = a; p < b; ++p) {
+        const uint32_t s = so[p];
+        if (s <= 1) {  // RUNA / RUNB digit
+            if (!inrun) {
+                inrun = true;
+                runpos = p;
+                run = 0;
+                inc = 1;
+            } else {
+                tv[p] = 0;
+            }
+            run += inc << s;
+            inc <<= 1;
+            if (run > smax) run = smax + 1;  // saturate (the total check reports it)
+            continue;
+        }
+        if (inrun) flush_run();
+        if (s >= eob) {  // end of block (always the last symbol)
+            tv[p] = 0;
+            continue;
+        }
+        const uint32_t r = s - 1;
+        uint32_t v, rr;
+        if (r < D) {
+            v = (L.rec[r >> 2][lane] >> (8 * (r & 3))) & 255u;
+            rr = r;
+        } else {
+            uint32_t kk = r - D;
+            v = 255u;
+            for (int w = 0; w < 8; ++w) {
+                const uint32_t u = L.used[w][lane];
+                const uint32_t z = 32u - (uint32_t)__popc(u);
+                if (kk < z) {
+                    v = (uint32_t)w * 32u + select_zero(u, kk);
+                    break;
+                }
+                kk -= z;
+            }
+            L.used[v >> 5][lane] |= 1u << (v & 31);
+            rr = D;
+            D++;
+        }
+        // entries [0, rr) move up one place, v goes to the front: words in
+        // groups of 8 (eight independent LDS reads in flight, then the shifts)
+        uint32_t carry = v;
+        const uint32_t wl = rr >> 2;
+        const uint32_t mlast = (rr & 3) == 3 ? 0xffffffffu : ((1u << (8 * ((rr & 3) + 1))) - 1u);
+        for (uint32_t g0 = 0; g0 <= wl; g0 += 8) {
+            uint32_t o[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = g0 + i <= wl ? L.rec[g0 + i][lane] : 0u;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t w = g0 + i;
+                if (w > wl) break;
+                const uint32_t sh = (o[i] << 8) | carry;
+                carry = o[i] >> 24;
+                L.rec[w][lane] = w < wl ? sh : ((sh & mlast) | (o[i] & ~mlast));
+            }
+        }
+        tv[p] = v | (1u << 8);
+        cnt += 1;
+    }
+    if (inrun) flush_run();
+    // the chunk's list permutation: recency entries, then untaken indices ascending
+    {
+        uint32_t pos = D;
+        for (int w = 0; w < 8 && pos < 256; ++w) {
+            uint32_t z = ~L.used[w][lane];
+            while (z && pos < 256) {
+                const uint32_t bit = (uint32_t)__builtin_ctz(z);
+                z &= z - 1;
+                const uint32_t e = (uint32_t)w * 32u + bit;
+                uint32_t& wd = L.rec[pos >> 2][lane];
+                const uint32_t sh = 8 * (pos & 3);
+                wd = (wd & ~(0xffu << sh)) | (e << sh);
+                pos++;
+            }
+        }
+    }
+    // ---- passes B + C, chunk by chunk with the whole wave: list_c (entries =
+    // output bytes; list_0 = the symbol map), then the chunk's bytes -- lanes
+    // take consecutive symbols, offsets by a wave scan of their byte counts --
+    // then list_{c+1}[i] = list_c[perm_c[i]]
+    const uint32_t incl = wave_incl_sum(cnt);
+    const uint32_t total = uniform((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+    const uint32_t cbase = incl - cnt;  // this lane's chunk offset
+    uint32_t status = total > smax ? (uint32_t)kDecSize : 0u;
+    const uint8_t* smp = symmaps + (size_t)k * 256;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L.lists[0][lane * 4 + j] = smp[lane * 4 + j];
+    __builtin_amdgcn_wave_barrier();
+    for (int c = 0; c < 64 && !status; ++c) {
+        const uint8_t* lc = L.lists[c & 1];
+        const uint32_t ca = uniform((uint32_t)__builtin_amdgcn_readlane((int)a, c));
+        const uint32_t cb = uniform((uint32_t)__builtin_amdgcn_readlane((int)b, c));
+        uint32_t o = uniform((uint32_t)__builtin_amdgcn_readlane((int)cbase, c));
+        for (uint32_t p0 = ca; p0 < cb; p0 += 64) {
+            const uint32_t p = p0 + (uint32_t)lane;
+            const uint32_t x = p < cb ? tv[p] : 0u;
+            const uint32_t n1 = x >> 8;
+            const uint32_t inc1 = wave_incl_sum(n1);
+            uint32_t q = o + inc1 - n1;
+            if (n1) {
+                const uint8_t byte = lc[x & 255u];
+                for (uint32_t r2 = 0; r2 < n1; ++r2) out[q + r2] = byte;
+            }
+            o += (uint32_t)__builtin_amdgcn_readlane((int)inc1, 63);
+        }
+        if (c < 63) {
+            uint32_t nv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t pi = (L.rec[lane][c] >> (8 * j)) & 255u;  // entry 4*lane + j of chunk c
+                nv[j] = lc[pi];
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < 4; ++j) L.lists[(c + 1) & 1][lane * 4 + j] = (uint8_t)nv[j];
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (status == 0 && orig >= total) status = kDecOrigPtr;
+    if (lane == 0) {
+        info->len = status == kDecSize ? 0u : total;
+        if (status) info->status = status;
     }
 }
 
@@ -455,7 +608,6 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
 constexpr int kWalkers = 1024;
 
 __global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict__ bwt, size_t stride,
-                                                       const uint32_t* __restrict__ hist,
                                                        const DecBlockInfo* __restrict__ infos,
                                                        const uint32_t* __restrict__ blocks, uint32_t nblocks,
                                                        uint32_t* __restrict__ merged, size_t mstride,
@@ -492,7 +644,7 @@ __global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict
     __syncthreads();
     {
         // thread t: byte t -> C[t] + counts of the earlier quarters
-        const uint32_t h = hist[(size_t)k * 256 + t];
+        const uint32_t h = base[0][t] + base[1][t] + base[2][t] + base[3][t];
         uint32_t total;
         const uint32_t cb = wg_excl_sum<256>(h, tmp, &total);
         const uint32_t c0 = base[0][t], c1 = base[1][t], c2 = base[2][t];

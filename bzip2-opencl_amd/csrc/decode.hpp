@@ -28,15 +28,20 @@ struct DecBlockInfo {
     uint64_t end_bit;  // first bit after the block (after its end-of-block symbol)
     uint32_t status;
     uint32_t orig;     // origPtr
-    uint32_t len;      // BWT (= RLE1) bytes
+    uint32_t len;      // BWT (= RLE1) bytes (dec_mtf_kernel)
     uint32_t crc;      // stored block CRC
+    uint32_t nsym;     // Huffman symbols, end-of-block included
+    uint32_t alpha;    // symbols in use (the end-of-block symbol is alpha + 1)
 };
 
 __global__ void dec_scan_kernel(const uint8_t* in, uint64_t n, DecCand* cand, uint32_t* ncand, uint32_t cap);
 __global__ void dec_huff_kernel(const uint8_t* in, uint64_t n, const DecCand* cand, const uint32_t* ids,
-                                uint32_t nids, uint32_t smax, uint32_t max_sel, uint8_t* bwt, size_t stride,
-                                uint8_t* selbuf, size_t sel_stride, uint32_t* hist_out, DecBlockInfo* infos);
-__global__ void dec_ibwt_kernel(const uint8_t* bwt, size_t stride, const uint32_t* hist, const DecBlockInfo* infos,
+                                uint32_t nids, uint32_t smax, uint32_t max_sel, uint16_t* syms, size_t sym_stride,
+                                uint8_t* symmap_out, DecBlockInfo* infos);
+__global__ void dec_mtf_kernel(const uint16_t* syms, size_t sym_stride, const uint8_t* symmaps,
+                               const uint32_t* blocks, uint32_t nblocks, uint32_t smax, uint32_t* scratch,
+                               size_t sstride, uint8_t* bwt, size_t stride, DecBlockInfo* infos);
+__global__ void dec_ibwt_kernel(const uint8_t* bwt, size_t stride, const DecBlockInfo* infos,
                                 const uint32_t* blocks, uint32_t nblocks, uint32_t* merged, size_t mstride,
                                 uint32_t* marks, size_t kstride, uint8_t* rle1, size_t rstride, uint32_t* bad);
 __global__ void dec_rle1_kernel(const uint8_t* rle1, size_t rstride, const DecBlockInfo* infos,

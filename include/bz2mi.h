@@ -146,9 +146,9 @@ int bz2mi_decompress(bz2mi_dctx* d, const uint8_t* in, size_t n, uint8_t* out, s
 int bz2mi_decompress_device(bz2mi_dctx* d, const void* d_in, size_t n, void* d_out, size_t cap, size_t* out_len,
                             void* hip_stream);
 
-/* milliseconds of the last call: [0] candidate scan, [1] Huffman + MTF + RLE2,
- * [2] inverse BWT, [3] RLE1 + CRC, [4] whole call */
-int bz2mi_dlast_timings(bz2mi_dctx* d, float* ms5);
+/* milliseconds of the last call: [0] candidate scan, [1] Huffman symbols,
+ * [2] MTF + RLE2 (and the stream walk), [3] inverse BWT, [4] RLE1 + CRC, [5] whole call */
+int bz2mi_dlast_timings(bz2mi_dctx* d, float* ms6);
 
 #ifdef __cplusplus
 }

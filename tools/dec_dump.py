@@ -17,8 +17,8 @@ try:
 except Exception as e:
     print("decode error:", e, flush=True)
 raw = open(path, "rb").read()
-end_bit, status, orig, ln, crc = struct.unpack("<QIIII", raw[:24])
-got = raw[24:]
+end_bit, status, orig, ln, crc, nsym, alpha = struct.unpack("<QIIIIII", raw[:32])
+got = raw[32:]
 blocks, _ = cr.split(data, 90000)
 bw, o = cr.bwt(blocks[0])
 print("status", status, "orig", orig, "want", o, "len", ln, "want", len(bw), "end_bit", end_bit, flush=True)
