@@ -52,7 +52,7 @@ int grow(T** p, size_t* cap, size_t count) {
 }  // namespace
 
 struct bz2mi_dctx {
-    int unit = 10000, device = 0;
+    int unit = 10000, device = 0, cus = 256;
     hipStream_t stream = nullptr;
     uint32_t* d_crctab = nullptr;
     uint32_t* d_cnt = nullptr;
@@ -95,6 +95,16 @@ struct bz2mi_dctx {
 };
 
 namespace {
+
+// inverse-BWT workgroups per CU (BZ2MI_IBWT_WG overrides, for experiments)
+int ibwt_wg_per_cu() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("BZ2MI_IBWT_WG");
+        v = (e && atoi(e) > 0) ? atoi(e) : 2;
+    }
+    return v;
+}
 
 // the whole decode of n bytes at d_in (4-byte aligned) into d_out
 int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, size_t cap, size_t* out_len,
@@ -282,7 +292,8 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
         if ((r = grow(&d->d_bad, &d->bad_cap, nb))) return r;
         DCHECK(hipMemsetAsync(d->d_bad, 0, nb * sizeof(uint32_t), s));
         DCHECK(hipMemcpyAsync(d->d_blocks, chain.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(dec_ibwt_kernel, dim3((unsigned)nb), dim3(256), 0, s, d->d_bwt, stride, d->d_info, d->d_blocks, (uint32_t)nb, d->d_merged, stride, d->d_marks, stride, d->d_rle1,
+        hipLaunchKernelGGL(dec_ibwt_kernel, dim3((unsigned)std::min<size_t>(nb, (size_t)d->cus * ibwt_wg_per_cu())),
+                           dim3(256), 0, s, d->d_bwt, stride, d->d_info, d->d_blocks, (uint32_t)nb, d->d_merged, stride, d->d_marks, stride, d->d_rle1,
                            stride, d->d_bad);
         DCHECK(hipGetLastError());
         DCHECK(hipEventRecord(d->ev[4], s));
@@ -360,6 +371,10 @@ bz2mi_dctx* bz2mi_dcreate(int unit, int device) {
     bz2mi_dctx* d = new bz2mi_dctx();
     d->unit = unit;
     d->device = device;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) d->cus = prop.multiProcessorCount;
+    }
     bool ok = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) == hipSuccess &&
               hipMalloc((void**)&d->d_crctab, 256 * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc((void**)&d->d_cnt, 4 * sizeof(uint32_t)) == hipSuccess &&

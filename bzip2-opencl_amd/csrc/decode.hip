@@ -601,26 +601,23 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
 // ---- K3: inverse BWT, one workgroup (256 threads) per block.  merged[r] =
 // (i << 8) | byte for the stable counting sort of the BWT bytes (BlockDecompressor
 // ::initialiseInverseBWT :233-262); the LF cycle from origPtr is the RLE1
-// block.  1024 walkers (4 per thread) start at evenly spaced rows (walker 0 at
+// block.  2048 walkers (8 per thread) start at evenly spaced rows (walker 0 at
 // origPtr), walk to the next start row (pass A: segment lengths and
 // successors), thread 0 chains the segments from walker 0, and the walkers
 // walk again writing their segment's bytes (pass B).
-constexpr int kWalkers = 1024;
+constexpr int kWPT = 8;               // walkers per thread
+constexpr int kWalkers = 256 * kWPT;  // per block
 
-__global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict__ bwt, size_t stride,
-                                                       const DecBlockInfo* __restrict__ infos,
-                                                       const uint32_t* __restrict__ blocks, uint32_t nblocks,
-                                                       uint32_t* __restrict__ merged, size_t mstride,
-                                                       uint32_t* __restrict__ marks, size_t kstride,
-                                                       uint8_t* __restrict__ rle1, size_t rstride,
-                                                       uint32_t* __restrict__ bad_out) {
+__device__ __forceinline__ void ibwt_one(uint32_t bi, const uint8_t* __restrict__ bwt, size_t stride,
+                                         const DecBlockInfo* __restrict__ infos, const uint32_t* __restrict__ blocks,
+                                         uint32_t* __restrict__ merged, size_t mstride, uint32_t* __restrict__ marks,
+                                         size_t kstride, uint8_t* __restrict__ rle1, size_t rstride,
+                                         uint32_t* __restrict__ bad_out) {
     __shared__ uint32_t base[4][256];
     __shared__ uint32_t seglen[kWalkers];
     __shared__ uint16_t succ[kWalkers];
     __shared__ uint32_t segoff[kWalkers];
     __shared__ uint32_t tmp[8];
-    const uint32_t bi = blockIdx.x;
-    if (bi >= nblocks) return;
     const uint32_t k = blocks[bi];  // decoded-candidate index
     const int t = threadIdx.x, w = wave_id(), lane = lane_id();
     const uint32_t n = infos[k].len;
@@ -688,12 +685,13 @@ __global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict
     }
     __threadfence_block();
     __syncthreads();
-    // pass A (4 walkers per thread, interleaved): one load per step -- the
-    // entry of the row just reached tells whether it starts a segment
-    uint32_t x[4], len[4], m[4];
-    bool act[4];
+    // pass A (kWPT walkers per thread): one load per walker and step -- the
+    // entry of the row just reached tells whether it starts a segment; the
+    // loads of all the thread's walkers are issued together
+    uint32_t x[kWPT], len[kWPT], m[kWPT];
+    bool act[kWPT];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kWPT; ++q) {
         const int j = t + 256 * q;
         act[q] = is_start(j);
         x[q] = start_of(j);
@@ -702,18 +700,24 @@ __global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict
     }
     bool any = true;
     while (any) {
-        any = false;
+        uint32_t nx[kWPT], mv[kWPT];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (!act[q]) continue;
-            len[q]++;
-            x[q] = (m[q] & 0x7fffffffu) >> 8;
-            if (x[q] >= n || len[q] > n) {  // inconsistent data: end the walker (never for valid blocks)
+        for (int q = 0; q < kWPT; ++q) {
+            nx[q] = (m[q] & 0x7fffffffu) >> 8;
+            if (act[q] && (nx[q] >= n || len[q] >= n)) {  // inconsistent data (never for valid blocks)
                 act[q] = false;
                 if (bad) *bad = 1u;
-                continue;
             }
-            m[q] = M[x[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < kWPT; ++q) mv[q] = act[q] ? M[nx[q]] : 0u;
+        any = false;
+#pragma unroll
+        for (int q = 0; q < kWPT; ++q) {
+            if (!act[q]) continue;
+            len[q]++;
+            x[q] = nx[q];
+            m[q] = mv[q];
             if (m[q] >> 31) {
                 act[q] = false;
                 seglen[t + 256 * q] = len[q];
@@ -741,9 +745,9 @@ __global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict
     }
     __syncthreads();
     // pass B: write the bytes of each segment
-    uint32_t o[4];
+    uint32_t o[kWPT];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kWPT; ++q) {
         const int j = t + 256 * q;
         act[q] = is_start(j);
         x[q] = start_of(j);
@@ -753,11 +757,14 @@ __global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict
     }
     any = true;
     while (any) {
+        uint32_t mv[kWPT];
+#pragma unroll
+        for (int q = 0; q < kWPT; ++q) mv[q] = len[q] ? M[x[q]] : 0u;
         any = false;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < kWPT; ++q) {
             if (!len[q]) continue;
-            const uint32_t mm = M[x[q]] & 0x7fffffffu;
+            const uint32_t mm = mv[q] & 0x7fffffffu;
             out[o[q]++] = (uint8_t)mm;
             x[q] = mm >> 8;
             if (x[q] >= n) len[q] = 1;
@@ -769,6 +776,23 @@ __global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict
         __threadfence_block();
         __syncthreads();
         for (uint32_t i = per + t; i < n; i += 256) out[i] = out[i % per];
+    }
+}
+
+// The grid is kept small (a few workgroups per CU, blocks taken in turn) so
+// that the merged vectors being walked at once stay in the 256 MB Infinity
+// Cache: the walks are random 4-byte loads, which from HBM would move a whole
+// line each.
+__global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict__ bwt, size_t stride,
+                                                       const DecBlockInfo* __restrict__ infos,
+                                                       const uint32_t* __restrict__ blocks, uint32_t nblocks,
+                                                       uint32_t* __restrict__ merged, size_t mstride,
+                                                       uint32_t* __restrict__ marks, size_t kstride,
+                                                       uint8_t* __restrict__ rle1, size_t rstride,
+                                                       uint32_t* __restrict__ bad_out) {
+    for (uint32_t bi = blockIdx.x; bi < nblocks; bi += gridDim.x) {
+        ibwt_one(bi, bwt, stride, infos, blocks, merged, mstride, marks, kstride, rle1, rstride, bad_out);
+        __syncthreads();
     }
 }
 
@@ -821,107 +845,100 @@ __global__ __launch_bounds__(256) void dec_rle1_kernel(const uint8_t* __restrict
     const uint32_t k = blocks[bi];
     const uint32_t n = infos[k].len;
     const uint8_t* X = rle1 + (size_t)bi * rstride;
-    const uint32_t c0 = (uint32_t)((uint64_t)n * t / 256), c1 = (uint32_t)((uint64_t)n * (t + 1) / 256);
-    if (pass == 0) {
-        // all five entry states in lockstep until they agree
-        uint32_t st[5] = {0, 1, 2, 3, 4}, ln[5] = {0, 0, 0, 0, 0};
-        uint32_t p = c0;
-        uint32_t prev = c0 ? X[c0 - 1] : 0xffffffffu;
-        bool same = false;
-        for (; p < c1 && !same; ++p) {
-            const uint32_t b = X[p];
+    // chunk bounds on 16-byte boundaries: every thread reads its chunk with
+    // 16-byte loads (the block buffer is 256-byte aligned and padded)
+    auto cbound = [&](uint32_t c) -> uint32_t {
+        return c == 0 ? 0u : (c >= 256 ? n : min(n, (uint32_t)((uint64_t)n * c / 256) & ~15u));
+    };
+    const uint32_t c0 = cbound(t), c1 = cbound(t + 1);
+    auto for_each_byte = [&](auto&& fn) {
+        for (uint32_t p = c0; p < c1; p += 16) {
+            const uint4 v = *reinterpret_cast<const uint4*>(X + p);
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t m = min(16u, c1 - p);
 #pragma unroll
-            for (int s = 0; s < 5; ++s) {
+            for (int j = 0; j < 16; ++j)
+                if ((uint32_t)j < m) fn((wv[j >> 2] >> (8 * (j & 3))) & 255u);
+        }
+    };
+    const uint32_t prev0 = c0 ? X[c0 - 1] : 0xffffffffu;
+    if (pass == 0) {
+        // all five entry states in lockstep until they agree, then one
+        uint32_t st[5] = {0, 1, 2, 3, 4}, ln[5] = {0, 0, 0, 0, 0};
+        uint32_t prev = prev0, s0 = 0, tail = 0;
+        bool same = false;
+        for_each_byte([&](uint32_t b) {
+            if (!same) {
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    uint32_t e;
+                    st[q] = rle1_next(st[q], b, prev, &e);
+                    ln[q] += e;
+                }
+                same = st[0] == st[1] && st[0] == st[2] && st[0] == st[3] && st[0] == st[4];
+                s0 = st[0];
+            } else {
                 uint32_t e;
-                st[s] = rle1_next(st[s], b, prev, &e);
-                ln[s] += e;
+                s0 = rle1_next(s0, b, prev, &e);
+                tail += e;
             }
             prev = b;
-            same = st[0] == st[1] && st[0] == st[2] && st[0] == st[3] && st[0] == st[4];
-        }
-        uint32_t s0 = st[0], tail = 0;
-        for (; p < c1; ++p) {
-            const uint32_t b = X[p];
-            uint32_t e;
-            s0 = rle1_next(s0, b, prev, &e);
-            tail += e;
-            prev = b;
-        }
-        for (int s = 0; s < 5; ++s) {
-            clen[t][s] = ln[s] + tail;
-            cexit[t][s] = same || c0 == c1 ? (c0 == c1 ? (uint32_t)s : s0) : st[s];
+        });
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            clen[t][q] = ln[q] + tail;
+            cexit[t][q] = c0 == c1 ? (uint32_t)q : (same ? s0 : st[q]);
         }
         __syncthreads();
         if (t == 0) {
-            uint32_t s = 0;
+            uint32_t sx = 0;
             uint64_t o = 0;
             for (int c = 0; c < 256; ++c) {
-                centry[c] = s;
+                centry[c] = sx;
                 coff[c] = o;
-                o += clen[c][s];
-                s = cexit[c][s];
+                o += clen[c][sx];
+                sx = cexit[c][sx];
             }
             coff[256] = o;
         }
         __syncthreads();
-        chunk_state[(size_t)bi * 256 + t] = centry[t];
+        // entry state and output offset of the chunk (offsets < 2^29: a block
+        // expands at most 259/5 times)
+        chunk_state[(size_t)bi * 256 + t] = centry[t] | (uint32_t)(coff[t] << 3);
         if (t == 0) out_len[bi] = coff[256];
         return;
     }
     // pass 1: write and CRC
     ctab[t] = crc_table[t];
-    const uint32_t entry = chunk_state[(size_t)bi * 256 + t];
+    const uint32_t cs = chunk_state[(size_t)bi * 256 + t];
     __syncthreads();
-    // chunk output offsets again (entry states known): lengths from one run
-    uint32_t st = entry, prev = c0 ? X[c0 - 1] : 0xffffffffu;
-    uint64_t len = 0;
-    for (uint32_t p = c0; p < c1; ++p) {
-        uint32_t e;
-        const uint32_t b = X[p];
-        st = rle1_next(st, b, prev, &e);
-        len += e;
-        prev = b;
-    }
-    cpart[t] = (uint32_t)len;
-    __syncthreads();
-    if (t == 0) {
-        uint64_t o = 0;
-        for (int c = 0; c < 256; ++c) {
-            coff[c] = o;
-            o += cpart[c];
-        }
-        coff[256] = o;
-    }
-    __syncthreads();
+    const uint64_t total = out_len[bi];
     const uint64_t base = out_off[bi];
-    uint64_t o = base + coff[t];
-    st = entry;
-    prev = c0 ? X[c0 - 1] : 0xffffffffu;
-    uint32_t runb = c0 >= 1 ? X[c0 - 1] : 0u;  // run byte for a count at the chunk start
-    uint32_t r = 0;                              // CRC register from 0
-    for (uint32_t p = c0; p < c1; ++p) {
-        const uint32_t b = X[p];
+    const uint64_t off = cs >> 3;
+    uint64_t o = base + off;
+    uint32_t st = cs & 7u, prev = prev0;
+    uint32_t r = 0;  // CRC register from 0
+    for_each_byte([&](uint32_t b) {
         uint32_t e;
         const uint32_t was = st;
         st = rle1_next(st, b, prev, &e);
-        const uint32_t ob = was == 4 ? runb : b;
+        const uint32_t ob = was == 4 ? prev : b;  // a count byte repeats the run byte before it
         for (uint32_t q = 0; q < e; ++q) {
             if (o < cap) out[o] = (uint8_t)ob;
             o++;
             r = (r << 8) ^ ctab[(r >> 24) ^ ob];
         }
-        if (was != 4) runb = b;
         prev = b;
-    }
+    });
     // block CRC: chunk registers shifted by the bytes after them
-    const uint64_t after = coff[256] - coff[t + 1];
+    const uint64_t after = total - (o - base);
     cpart[t] = crc_shift(r, after);
     __syncthreads();
     if (t < 64) {
         uint32_t v = cpart[t] ^ cpart[t + 64] ^ cpart[t + 128] ^ cpart[t + 192];
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d);
-        if (t == 0) crc_out[bi] = ~(v ^ crc_shift(0xffffffffu, coff[256]));
+        if (t == 0) crc_out[bi] = ~(v ^ crc_shift(0xffffffffu, total));
     }
 }
 
