@@ -48,6 +48,24 @@ def ensure_built():
         subprocess.run(["make", "-C", PKG, "-j8"], check=True, stdout=subprocess.DEVNULL)
 
 
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r01_traffic.json")
+
+
+def stage_traffic(args, stage):
+    """HBM-side bytes per launch of `stage` from the committed rocprofv3 --pmc
+    passes of this same command (tools/round_profile.sh -> tools/traffic.py:
+    FETCH_SIZE x2 per the gfx950 note of MI355X_MICROARCH.md, + WRITE_SIZE).
+    Only for the workload those passes ran (C2 at the default level/p/unit)."""
+    if args.data != "random" or args.mib != 1024 or args.level != 9 or args.parallel != 10 or args.unit != 10000:
+        return None, None
+    try:
+        with open(TRAFFIC_PROFILE) as f:
+            prof = json.load(f)
+        return int(prof["stages"][stage]["traffic_bytes"]), os.path.relpath(TRAFFIC_PROFILE, REPO)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def cpu_baseline(sample_bytes: int) -> dict:
     """Reference compressor (O_ref = the reference's own kernel.cpp + host code,
     oracle/_ref/liboref.so) or, where it was not built, the C restatement
@@ -201,8 +219,9 @@ def main():
     }
     dom = max((k for k in alg if avg.get(k, 0) > 0), key=lambda k: avg[k])
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9
+    traffic, tsrc = stage_traffic(args, dom)
     roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
             "algorithmic_bytes": int(alg[dom]), "avg_ms": round(avg[dom], 3),
             "pipeline_GBps": round((n + out_len) / (ms_step * 1e-3) / 1e9, 2),
             "stage_ms": {k: round(v, 3) for k, v in avg.items()}}

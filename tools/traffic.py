@@ -1,0 +1,39 @@
+"""Per-launch HBM-side traffic of the bz2mi kernels from tools/round_profile.sh's
+two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; kB per dispatch).
+
+The bench command of those passes runs 2 compressions (1 warmup + 1 step);
+every kernel's counters are averaged over its dispatches per compression.
+FETCH_SIZE is doubled as /opt/skills/guides/MI355X_MICROARCH.md prescribes for
+gfx950 (it reports half the bytes of wide coalesced reads); WRITE_SIZE is
+taken as is.  Both count Infinity-Cache traffic too (the guide).  Writes
+profiles/<name>.json, read by bench.py for the `traffic` field."""
+import collections
+import csv
+import json
+import sys
+
+src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/round"
+dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01_traffic.json"
+steps = 2
+per = collections.defaultdict(lambda: {"fetch_bytes": 0.0, "write_bytes": 0.0, "dispatches": 0})
+for counter, sub, scale in (("FETCH_SIZE", "pmc_fetch", 2.0), ("WRITE_SIZE", "pmc_write", 1.0)):
+    for r in csv.DictReader(open(f"{src}/{sub}/run_counter_collection.csv")):
+        if "bz2mi::" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
+            continue
+        k = r["Kernel_Name"].split("(")[0].replace("bz2mi::", "")
+        key = "fetch_bytes" if counter == "FETCH_SIZE" else "write_bytes"
+        per[k][key] += float(r["Counter_Value"]) * 1024.0 * scale / steps
+        if counter == "FETCH_SIZE":
+            per[k]["dispatches"] += 1
+stages = {"front": ["fe_"], "bwt": ["bwt_"], "mtf": ["mtf_kernel"], "huffman": ["huffman_kernel"],
+          "assemble": ["assemble", "offsets_dev", "advance"]}
+out = {"command": "python3 bench.py --no-cpu --no-verify --steps 1 --warmup 1 (C2, 1 GiB random, -9, p=10)",
+       "workload": "C2", "note": "bytes per compression of the 1 GiB input; FETCH_SIZE x2 (gfx950 correction)",
+       "kernels": {k: {a: round(b) for a, b in v.items()} for k, v in sorted(per.items())},
+       "stages": {}}
+for st, pre in stages.items():
+    f = sum(v["fetch_bytes"] for k, v in per.items() if any(k.startswith(p) for p in pre))
+    w = sum(v["write_bytes"] for k, v in per.items() if any(k.startswith(p) for p in pre))
+    out["stages"][st] = {"fetch_bytes": round(f), "write_bytes": round(w), "traffic_bytes": round(f + w)}
+json.dump(out, open(dst, "w"), indent=1)
+print(json.dumps(out["stages"], indent=1))
