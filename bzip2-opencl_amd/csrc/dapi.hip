@@ -66,6 +66,8 @@ struct bz2mi_dctx {
     size_t syms_cap = 0;
     uint8_t* d_symmap = nullptr;
     size_t symmap_cap = 0;
+    uint8_t* d_tabs = nullptr;
+    size_t tabs_cap = 0;
     bz2mi::DecBlockInfo* d_info = nullptr;
     size_t info_cap = 0;
     uint32_t* d_blocks = nullptr;
@@ -150,11 +152,15 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
     if ((r = grow(&d->d_ids, &d->ids_cap, nk))) return r;
     if ((r = grow(&d->d_syms, &d->syms_cap, nk * sym_stride))) return r;
     if ((r = grow(&d->d_symmap, &d->symmap_cap, nk * 256))) return r;
+    if ((r = grow(&d->d_tabs, &d->tabs_cap, nk * kTabBytes))) return r;
     if ((r = grow(&d->d_info, &d->info_cap, nk))) return r;
     if (nk) {
         DCHECK(hipMemcpyAsync(d->d_ids, ids.data(), nk * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(dec_huff_kernel, dim3((unsigned)nk), dim3(64), (max_sel + 7) / 8 * 4, s, d_in, (uint64_t)n, d->d_cand,
-                           d->d_ids, (uint32_t)nk, smax, max_sel, d->d_syms, sym_stride, d->d_symmap, d->d_info);
+        hipLaunchKernelGGL(dec_huff_kernel, dim3((unsigned)nk), dim3(64), (max_sel + 7) / 8 * 4, s, d_in, (uint64_t)n,
+                           d->d_cand, d->d_ids, (uint32_t)nk, max_sel, d->d_tabs, d->d_symmap, d->d_info);
+        DCHECK(hipGetLastError());
+        hipLaunchKernelGGL(dec_sym_kernel, dim3((unsigned)((nk + kDecSymBlocks - 1) / kDecSymBlocks)), dim3(64), 0, s, d_in, (uint64_t)n, d->d_tabs,
+                           (uint32_t)nk, smax, d->d_syms, sym_stride, d->d_info);
         DCHECK(hipGetLastError());
     }
     std::vector<DecBlockInfo> info(nk);
@@ -409,7 +415,7 @@ void bz2mi_ddestroy(bz2mi_dctx* d) {
     (void)hipSetDevice(d->device);
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     for (void* p : {(void*)d->d_crctab, (void*)d->d_cnt, (void*)d->d_cand, (void*)d->d_ids, (void*)d->d_bwt,
-                    (void*)d->d_syms, (void*)d->d_symmap, (void*)d->d_info, (void*)d->d_blocks, (void*)d->d_merged,
+                    (void*)d->d_syms, (void*)d->d_symmap, (void*)d->d_tabs, (void*)d->d_info, (void*)d->d_blocks, (void*)d->d_merged,
                     (void*)d->d_marks, (void*)d->d_rle1, (void*)d->d_cstate, (void*)d->d_olen, (void*)d->d_ooff,
                     (void*)d->d_crc, (void*)d->d_in, (void*)d->d_out})
         if (p) (void)hipFree(p);

@@ -81,6 +81,8 @@ struct BitReader {
         return x;
     }
     __device__ __forceinline__ uint64_t load64(uint64_t i) const {
+        if ((i + 2) * 4 <= (nbits >> 3))
+            return ((uint64_t)__builtin_bswap32(w[i]) << 32) | __builtin_bswap32(w[i + 1]);
         return ((uint64_t)word(i) << 32) | word(i + 1);
     }
     __device__ void init(const uint8_t* base, uint64_t nbytes, uint64_t bitpos) {
@@ -194,12 +196,11 @@ __global__ __launch_bounds__(256) void dec_scan_kernel(const uint8_t* __restrict
 }
 
 // ---- K2: one wave per candidate block: header, symbol map, selectors, code
-// lengths, decoding tables, then the Huffman symbols.  `smax` bounds the BWT
-// bytes a block may hold (the largest digit x unit).
+// lengths and the decoding tables (HuffmanStageDecoder::
+// createHuffmanDecodingTables :86-135), handed to dec_sym_kernel in `tabs`.
 __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict__ in, uint64_t n,
                                                       const DecCand* __restrict__ cand, const uint32_t* __restrict__ ids,
-                                                      uint32_t nids, uint32_t smax, uint32_t max_sel,
-                                                      uint16_t* __restrict__ syms, size_t sym_stride,
+                                                      uint32_t nids, uint32_t max_sel, uint8_t* __restrict__ tabs,
                                                       uint8_t* __restrict__ symmap_out,
                                                       DecBlockInfo* __restrict__ infos) {
     __shared__ HuffLds L;
@@ -216,6 +217,8 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
         info->end_bit = 0;
         info->len = 0;
         info->nsym = 0;
+        info->data_bit = 0;
+        info->nsel = 0;
     }
     const uint32_t crc = br.bits(16) << 16;
     const uint32_t crc2 = crc | br.bits(16);
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
                 }
         }
     }
-    const uint32_t eob = nsym + 1, alpha = nsym + 2;
+    const uint32_t alpha = nsym + 2;  // symbols 0 (RUNA) .. nsym + 1 (end of block)
     const uint32_t ntab = br.bits(3), nsel = br.bits(15);
     if (ntab < 2 || ntab > (uint32_t)kMaxTables || nsel < 1 || nsel > max_sel || nsel > (uint32_t)kDecMaxSel) {
         fail(info, kDecTables);
@@ -331,43 +334,104 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
         fail(info, kDecRandomised);
         return;
     }
-    // ---- data, part 1: the Huffman symbols (HuffmanStageDecoder::nextSymbol
-    // :48-71), the only serial chain of the block: one LDS lookup and a few
-    // scalar operations per symbol.  Symbols are gathered 64 at a time in a
-    // VGPR (v_writelane) and stored coalesced; MTF / RLE2 are dec_mtf_kernel's.
-    uint32_t g = 0, gpos = 0;
-    auto sel_at = [&](uint32_t i) -> uint32_t { return uniform((sel_lds[i >> 3] >> (4 * (i & 7))) & 15u); };
-    uint32_t table = sel_at(0);
-    uint32_t status = 0;
-    uint32_t ns = 0;       // symbols decoded
-    uint32_t chunk = 0;    // symbol ns & 63 of the current chunk in lane ns & 63
+    // ---- hand the tables to dec_sym_kernel: lookup tables, limits, bases,
+    // permutations and the selectors, and where the data starts
+    uint8_t* tb = tabs + (size_t)k * kTabBytes;
+    {
+        uint32_t* d32 = reinterpret_cast<uint32_t*>(tb);
+        const uint32_t* l32 = reinterpret_cast<const uint32_t*>(&L.lut[0][0]);
+        for (int i = lane; i < kMaxTables * (1 << kLutBits) / 2; i += 64) d32[i] = l32[i];
+        int32_t* lim = reinterpret_cast<int32_t*>(tb + kTabLimit);
+        int32_t* bas = reinterpret_cast<int32_t*>(tb + kTabBase);
+        for (int i = lane; i < kMaxTables * (kMaxDecLen + 2); i += 64) {
+            lim[i] = (&L.limit[0][0])[i];
+            bas[i] = (&L.base[0][0])[i];
+        }
+        uint16_t* per = reinterpret_cast<uint16_t*>(tb + kTabPerm);
+        for (int i = lane; i < kMaxTables * kMaxAlpha; i += 64) per[i] = (&L.perm[0][0])[i];
+        uint8_t* sg = tb + kTabSel;
+        for (uint32_t i = lane; i < nsel; i += 64) sg[i] = (uint8_t)((sel_lds[i >> 3] >> (4 * (i & 7))) & 15u);
+    }
+    if (lane == 0) {
+        info->status = 0;
+        info->data_bit = br.pos;
+        info->nsel = nsel;
+        info->alpha = nsym;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) symmap_out[(size_t)k * 256 + lane * 4 + j] = L.symmap[lane * 4 + j];
+}
+
+// ---- K2s: the Huffman symbols (HuffmanStageDecoder::nextSymbol :48-71), the
+// one serial chain of a block: lanes 0..kSymBlocks-1 of a wave each decode
+// their own block, with its lookup tables in LDS (one gather per symbol) and
+// a private bit reader; the other lanes only stage the tables.  Vector code:
+// the chains of 8 blocks per wave share the instruction stream instead of
+// queueing on the CU's one scalar unit.
+#ifndef BZ2MI_SYM_BLOCKS
+#define BZ2MI_SYM_BLOCKS 2
+#endif
+constexpr int kSymBlocks = BZ2MI_SYM_BLOCKS;  // blocks per wave (LDS: 6 KB of tables each; 2 measured best
+                                              // of 1/2/4/8: 73 / 91 / 94 / 90 ms per GiB at 2/1/4/8)
+
+// codes longer than the lookup table (the reference's limit / base walk)
+__device__ __forceinline__ uint32_t long_code(const BitReader& br, const int32_t* lim, const int32_t* bas,
+                                           const uint16_t* per, uint32_t* len_out) {
+    for (uint32_t len = kLutBits + 1; len <= (uint32_t)kMaxDecLen; ++len) {
+        const int32_t cv = (int32_t)br.peek((int)len);
+        if (cv <= lim[len]) {
+            *len_out = len;
+            return per[(uint32_t)(cv + bas[len])];
+        }
+    }
+    *len_out = 0;
+    return 0xffffffffu;
+}
+
+__global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                     const uint8_t* __restrict__ tabs, uint32_t nids, uint32_t smax,
+                                                     uint16_t* __restrict__ syms, size_t sym_stride,
+                                                     DecBlockInfo* __restrict__ infos) {
+    __shared__ uint16_t lut[kSymBlocks][kMaxTables * (1 << kLutBits)];
+    const int lane = lane_id();
+    const uint32_t k0 = blockIdx.x * kSymBlocks;
+    // stage the lookup tables of this wave's blocks
+    for (int b = 0; b < kSymBlocks; ++b) {
+        if (k0 + b >= nids) break;
+        const uint32_t st = uniform(infos[k0 + b].status);
+        if (st) continue;
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(tabs + (size_t)(k0 + b) * kTabBytes);
+        uint32_t* d32 = reinterpret_cast<uint32_t*>(&lut[b][0]);
+        for (int i = lane; i < kMaxTables * (1 << kLutBits) / 2; i += 64) d32[i] = s32[i];
+    }
+    __syncthreads();
+    const uint32_t k = k0 + (uint32_t)lane;
+    if (lane >= kSymBlocks || k >= nids) return;
+    DecBlockInfo* info = infos + k;
+    if (info->status) return;
+    const uint8_t* tb = tabs + (size_t)k * kTabBytes;
+    const int32_t* lim = reinterpret_cast<const int32_t*>(tb + kTabLimit);
+    const int32_t* bas = reinterpret_cast<const int32_t*>(tb + kTabBase);
+    const uint16_t* per = reinterpret_cast<const uint16_t*>(tb + kTabPerm);
+    const uint8_t* sg = tb + kTabSel;
+    const uint32_t nsel = info->nsel, eob = info->alpha + 1;
+    const uint16_t* L = &lut[lane][0];
+    BitReader br;
+    br.init(in, n, info->data_bit);
     uint16_t* so = syms + (size_t)k * sym_stride;
     const uint32_t ns_max = smax + 2;
+    uint32_t g = 0, gleft = kGroupRun, ns = 0, status = 0;
+    uint32_t tbase = (uint32_t)sg[0] << kLutBits;
+    uint32_t nsel1 = nsel > 1 ? sg[1] : 0u;  // next group's table, loaded ahead
     for (;;) {
-        if (gpos == (uint32_t)kGroupRun) {
-            if (++g >= nsel) {
-                status = kDecData;
-                break;
-            }
-            table = sel_at(g);
-            gpos = 0;
-        }
-        gpos++;
-        const uint32_t e = uniform(L.lut[table][br.peek(kLutBits)]);
+        const uint32_t e = L[tbase + br.peek(kLutBits)];
         uint32_t sym, len;
         if (e != kLong) {
             sym = e & 0xfffu;
             len = e >> 12;
         } else {
-            len = kLutBits + 1;
-            sym = 0xffffffffu;
-            for (; len <= (uint32_t)kMaxDecLen; ++len) {
-                const int32_t cv = (int32_t)br.peek((int)len);
-                if (cv <= L.limit[table][len]) {
-                    sym = L.perm[table][cv + L.base[table][len]];
-                    break;
-                }
-            }
+            const uint32_t t = tbase >> kLutBits;
+            sym = long_code(br, lim + t * (kMaxDecLen + 2), bas + t * (kMaxDecLen + 2), per + t * kMaxAlpha, &len);
             if (sym == 0xffffffffu) {
                 status = kDecData;
                 break;
@@ -378,24 +442,25 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
             status = kDecData;
             break;
         }
-        chunk = (uint32_t)lane == (ns & 63u) ? sym : chunk;
-        ns++;
-        if ((ns & 63u) == 0) so[ns - 64 + lane] = (uint16_t)chunk;
+        so[ns++] = (uint16_t)sym;
         if (sym == eob) break;
         if (ns >= ns_max) {
             status = kDecSize;
             break;
         }
+        if (--gleft == 0) {  // next group of 50 (HuffmanStageDecoder.hpp:50-57)
+            if (++g >= nsel) {
+                status = kDecData;
+                break;
+            }
+            tbase = nsel1 << kLutBits;
+            nsel1 = g + 1 < nsel ? sg[g + 1] : 0u;
+            gleft = kGroupRun;
+        }
     }
-    if ((ns & 63u) && (uint32_t)lane < (ns & 63u)) so[(ns & ~63u) + lane] = (uint16_t)chunk;
-    if (lane == 0) {
-        info->status = status;
-        info->nsym = ns;
-        info->alpha = nsym;
-        info->end_bit = br.pos;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) symmap_out[(size_t)k * 256 + lane * 4 + j] = L.symmap[lane * 4 + j];
+    info->status = status;
+    info->nsym = ns;
+    info->end_bit = br.pos;
 }
 
 // ---- K2b: data, part 2 (BlockDecompressor::decodeHuffmanData :177-231):

@@ -32,12 +32,30 @@ struct DecBlockInfo {
     uint32_t crc;      // stored block CRC
     uint32_t nsym;     // Huffman symbols, end-of-block included
     uint32_t alpha;    // symbols in use (the end-of-block symbol is alpha + 1)
+    uint64_t data_bit; // first bit of the Huffman data (after the tables)
+    uint32_t nsel;     // selectors
+    uint32_t pad;
 };
+
+// per-candidate decoding tables (dec_huff_kernel -> dec_sym_kernel): 9-bit
+// lookup tables, limits and bases per code length, symbol permutations,
+// selectors
+constexpr size_t kTabLimit = 6 * 512 * 2;                 // after the lookup tables
+constexpr size_t kTabBase = kTabLimit + 6 * 25 * 4;
+constexpr size_t kTabPerm = kTabBase + 6 * 25 * 4;
+constexpr size_t kTabSel = kTabPerm + 6 * 258 * 2 + 8;    // (8: alignment pad)
+constexpr size_t kTabBytes = (kTabSel + 18002 + 255) & ~(size_t)255;
 
 __global__ void dec_scan_kernel(const uint8_t* in, uint64_t n, DecCand* cand, uint32_t* ncand, uint32_t cap);
 __global__ void dec_huff_kernel(const uint8_t* in, uint64_t n, const DecCand* cand, const uint32_t* ids,
-                                uint32_t nids, uint32_t smax, uint32_t max_sel, uint16_t* syms, size_t sym_stride,
-                                uint8_t* symmap_out, DecBlockInfo* infos);
+                                uint32_t nids, uint32_t max_sel, uint8_t* tabs, uint8_t* symmap_out,
+                                DecBlockInfo* infos);
+#ifndef BZ2MI_SYM_BLOCKS
+#define BZ2MI_SYM_BLOCKS 2
+#endif
+constexpr int kDecSymBlocks = BZ2MI_SYM_BLOCKS;  // blocks per wave of dec_sym_kernel
+__global__ void dec_sym_kernel(const uint8_t* in, uint64_t n, const uint8_t* tabs, uint32_t nids, uint32_t smax,
+                               uint16_t* syms, size_t sym_stride, DecBlockInfo* infos);
 __global__ void dec_mtf_kernel(const uint16_t* syms, size_t sym_stride, const uint8_t* symmaps,
                                const uint32_t* blocks, uint32_t nblocks, uint32_t smax, uint32_t* scratch,
                                size_t sstride, uint8_t* bwt, size_t stride, DecBlockInfo* infos);
