@@ -688,11 +688,12 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
         bz2mi_destroy(c);
         return nullptr;
     }
-    // Batches of about 1.5 GB of block input (BZ2MI_BATCH_BLOCKS overrides).
-    // Measured on MI355X: the stage kernels are throughput-bound, so running
-    // them concurrently on smaller batches (the three-stream pipeline) was
-    // slower (1 GiB random: 17.1 GB/s in one batch, 16.2 in four, 15.3 in
-    // eight); the pipeline matters for inputs larger than one batch.
+    // Batches of about 1.5 GB of block input (BZ2MI_BATCH_BLOCKS overrides),
+    // run through the three-stream pipeline when the input is larger.
+    // Measured on MI355X, 1 GiB random: one batch 24.6 GB/s, batches of 3000
+    // blocks 25.1, 2400 25.3, 2000 24.5, 1000 21.8 (before the staged BWT
+    // scatter); after it one batch and batches of 3072 both give 26.0 -- one
+    // batch keeps the per-stage event times per launch (the roofline figures).
     c->batch_blocks = std::min(16384, std::max(64, (int)((1536u << 20) / (unsigned)c->S)));
     if (const char* e = getenv("BZ2MI_BATCH_BLOCKS")) c->batch_blocks = std::max(1, atoi(e));
     for (auto& e : c->ev) (void)hipEventCreate(&e);

@@ -491,7 +491,7 @@ __device__ void wg_sort_group(Scratch& s, Seg seg, BwtShared& sh, Seg* out, uint
 // ---- phase 1a: counting sort of the rotations by their first byte into sa.
 // Thread t gets bucket t: start *ex, size *c.
 __device__ void count_sort_first(const uint8_t* __restrict__ T, int n, uint32_t* __restrict__ sa, BwtShared& sh,
-                                 uint32_t* c_out, uint32_t* ex_out) {
+                                 uint32_t* c_out, uint32_t* ex_out, uint32_t* stage, uint32_t* th, uint32_t* ts) {
     const int t = threadIdx.x;
     sh.hist[t] = 0;
     __syncthreads();
@@ -511,15 +511,42 @@ __device__ void count_sort_first(const uint8_t* __restrict__ T, int n, uint32_t*
     const uint32_t ex = wg_excl_sum<NT>(c, sh.tmp, &total);
     sh.base[t] = ex;
     __syncthreads();
-    for (int v = t; v < n16; v += NT) {
-        const uint4 w = T4[v];
-        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+    // scatter, staged per tile of 4096 rotations: ranks inside the tile by
+    // LDS atomics, the tile ordered by first byte in LDS, then written out as
+    // runs (consecutive threads -> consecutive SA slots of a bucket) instead
+    // of one scattered 4-byte store per rotation
+    for (int tile0 = 0; tile0 < n; tile0 += NT * 16) {
+        th[t] = 0;
+        __syncthreads();
+        const int i0 = tile0 + t * 16;
+        uint32_t bv[16], rk[16];
+        if (i0 + 16 <= n) {
+            const uint4 w = T4[i0 >> 4];
+            const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) bv[k] = (ww[k >> 2] >> ((k & 3) * 8)) & 255u;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) bv[k] = i0 + k < n ? T[i0 + k] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rk[k] = i0 + k < n ? atomicAdd(&th[bv[k]], 1u) : 0u;
+        __syncthreads();
+        uint32_t tn;
+        ts[t] = wg_excl_sum<NT>(th[t], sh.tmp, &tn);
+        __syncthreads();
 #pragma unroll
         for (int k = 0; k < 16; ++k)
-            sa[atomicAdd(&sh.base[(ww[k >> 2] >> ((k & 3) * 8)) & 255u], 1u)] = (uint32_t)(v * 16 + k);
+            if (i0 + k < n) stage[ts[bv[k]] + rk[k]] = (uint32_t)(i0 + k) | (bv[k] << 24);
+        __syncthreads();
+        for (uint32_t j = t; j < tn; j += NT) {
+            const uint32_t v = stage[j], b = v >> 24;
+            sa[sh.base[b] + (j - ts[b])] = v & 0xffffffu;
+        }
+        __syncthreads();
+        sh.base[t] += th[t];
+        __syncthreads();
     }
-    for (int i = (n16 << 4) + t; i < n; i += NT) sa[atomicAdd(&sh.base[T[i]], 1u)] = (uint32_t)i;
-    __syncthreads();
     *c_out = c;
     *ex_out = ex;
 }
@@ -1119,6 +1146,7 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
                                                          BwtItem* __restrict__ lq, uint32_t* __restrict__ lcount,
                                                          size_t lcap, uint32_t* __restrict__ present_out) {
     __shared__ BwtShared sh;
+    __shared__ uint32_t stage[NT * 16], th[256], ts[256];
     const int b = blockIdx.x;
     if (b >= nblocks) return;
     const int t = threadIdx.x;
@@ -1135,7 +1163,7 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
     }
     uint32_t* sa = sa_all + (size_t)b * stride;
     uint32_t c, ex;
-    count_sort_first(T, n, sa, sh, &c, &ex);
+    count_sort_first(T, n, sa, sh, &c, &ex, stage, th, ts);
     {  // symbols in use (the MTF symbol map): bit t of the 256-bit set
         const uint64_t m = __ballot(c != 0);
         if (lane_id() == 0) {

@@ -371,8 +371,8 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
 #ifndef BZ2MI_SYM_BLOCKS
 #define BZ2MI_SYM_BLOCKS 2
 #endif
-constexpr int kSymBlocks = BZ2MI_SYM_BLOCKS;  // blocks per wave (LDS: 6 KB of tables each; 2 measured best
-                                              // of 1/2/4/8: 73 / 91 / 94 / 90 ms per GiB at 2/1/4/8)
+constexpr int kSymBlocks = BZ2MI_SYM_BLOCKS;  // blocks per wave (LDS: 6 KB of tables each); measured
+                                              // 1/2/4/8 blocks: 91 / 73 / 94 / 90 ms per GiB
 
 // codes longer than the lookup table (the reference's limit / base walk)
 __device__ __forceinline__ uint32_t long_code(const BitReader& br, const int32_t* lim, const int32_t* bas,
