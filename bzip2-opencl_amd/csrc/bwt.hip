@@ -695,9 +695,10 @@ __device__ __forceinline__ void wave_sort_lds_any(const uint8_t* __restrict__ T,
     else wave_sort_lds<8>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
 }
 
+// `pre`: the batch's SA entries, loaded ahead by the caller (entry e*64+lane in pre[e])
 __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
                                   const GroupSink& sink, uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
-                                  Bucket2Lds& L) {
+                                  Bucket2Lds& L, const uint32_t (&pre)[kSmall / 64]) {
     constexpr int E = kSmall / 64;
     const int lane = lane_id();
 #pragma unroll
@@ -712,7 +713,7 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
             ii[e] = 0;
             key[e] = 0;
             if (g < seg.len) {
-                const uint32_t i = s.sa[seg.start + g];
+                const uint32_t i = pre[e];
                 uint32_t p = i + d;
                 if (p >= (uint32_t)n) p %= (uint32_t)n;
                 key[e] = load8(T, n, p);
@@ -1300,17 +1301,45 @@ __global__ __launch_bounds__(256, 4) void bwt_small_kernel(const uint8_t* __rest
     // XCD-aware split of the queue (see bwt_level_kernel)
     const uint32_t xcd = blockIdx.x % kXcds, nwaves = gridDim.x / kXcds * (NT / 64);
     const uint32_t qlo = (uint32_t)((uint64_t)nq * xcd / kXcds), qhi = (uint32_t)((uint64_t)nq * (xcd + 1) / kXcds);
-    for (uint32_t q = qlo + blockIdx.x / kXcds * (NT / 64) + wave_id(); q < qhi; q += nwaves) {
-        const uint64_t e = squeue[shard_locate(si, uniform(q), scap)];
+    // software pipeline over the wave's batches: the queue entry two batches
+    // ahead and the SA entries (and block length) of the next batch are
+    // loaded while the current one is sorted, so a batch waits for one
+    // memory round trip (its text gathers) instead of three
+    constexpr int E = kSmall / 64;
+    const int lane = lane_id();
+    auto entry = [&](uint32_t q) -> uint64_t { return q < qhi ? squeue[shard_locate(si, uniform(q), scap)] : 0ull; };
+    auto load_batch = [&](uint64_t e, uint32_t (&sa)[E], uint32_t& n) {
         const uint32_t b = uniform((uint32_t)(e >> 42));
-        const Seg seg{uniform((uint32_t)(e >> 22) & 0xfffffu), uniform((uint32_t)(e >> 13) & 511u) + 1u};
-        const uint32_t d = uniform((uint32_t)e & 0x1fffu);
-        const int n = (int)uniform(lens[b]);
+        const uint32_t start = uniform((uint32_t)(e >> 22) & 0xfffffu), len = uniform((uint32_t)(e >> 13) & 511u) + 1u;
+        n = lens[b];
+        const uint32_t* sab = sa_all + (size_t)b * stride + start;
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            const uint32_t g = (uint32_t)(k * 64 + lane);
+            sa[k] = g < len ? sab[g] : 0u;
+        }
+    };
+    uint32_t q = qlo + blockIdx.x / kXcds * (NT / 64) + wave_id();
+    uint64_t ec = entry(q), en = entry(q + nwaves);
+    uint32_t sac[E], nc = 0;
+    if (q < qhi) load_batch(ec, sac, nc);
+    for (; q < qhi; q += nwaves) {
+        uint32_t san[E], nn = 0;
+        if (q + nwaves < qhi) load_batch(en, san, nn);
+        const uint64_t enn = entry(q + 2 * nwaves);
+        const uint32_t b = uniform((uint32_t)(ec >> 42));
+        const Seg seg{uniform((uint32_t)(ec >> 22) & 0xfffffu), uniform((uint32_t)(ec >> 13) & 511u) + 1u};
+        const uint32_t d = uniform((uint32_t)ec & 0x1fffu);
         Scratch s{};
         s.sa = sa_all + (size_t)b * stride;
         const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, b, tl + (size_t)b * tcap, tcount + b};
-        wave_sort_bucket2(blocks + (size_t)b * stride, n, s, seg, d, sink, bwt_out + (size_t)b * stride, orig_out + b,
-                          lds[wave_id()]);
+        wave_sort_bucket2(blocks + (size_t)b * stride, (int)uniform(nc), s, seg, d, sink, bwt_out + (size_t)b * stride,
+                          orig_out + b, lds[wave_id()], sac);
+#pragma unroll
+        for (int k = 0; k < E; ++k) sac[k] = san[k];
+        nc = nn;
+        ec = en;
+        en = enn;
     }
 }
 
