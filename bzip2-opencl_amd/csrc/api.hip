@@ -117,6 +117,8 @@ struct bz2mi_ctx {
     int small_grid = 0;                             // resident workgroups of bwt_small_kernel
     int level_slots = 0;                            // resident workgroups of bwt_level_kernel
     uint8_t* d_lscratch = nullptr;                  // their scratch slots
+    int wlevel_grid = 0;                            // resident workgroups of bwt_wlevel_kernel
+    uint32_t* d_lspill = nullptr;                   // wave-level stage spill (one word per rotation of a batch)
     int bwtq_blocks = 0;           // capacity of the queues in blocks
     uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
     uint32_t* d_crctab = nullptr;
@@ -238,12 +240,13 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     if (nb > c->bwtq_blocks) {  // queues are shared by the batches: BWTs run one at a time
         HIPCHECK(hipStreamSynchronize(s));
         for (void* p : {(void*)c->d_sq, (void*)c->d_lq[0], (void*)c->d_lq[1], (void*)c->d_tq[0], (void*)c->d_tq[1],
-                        (void*)c->d_tc})
+                        (void*)c->d_tc, (void*)c->d_lspill})
             if (p) (void)hipFree(p);
         c->d_sq = nullptr;
         c->d_lq[0] = c->d_lq[1] = nullptr;
         c->d_tq[0] = c->d_tq[1] = nullptr;
         c->d_tc = nullptr;
+        c->d_lspill = nullptr;
         c->bwtq_blocks = 0;
         const size_t B = (size_t)std::max(nb, 16);
         const size_t Bs = (B + kBwtShards - 1) / kBwtShards;  // blocks per shard
@@ -254,6 +257,7 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         if ((r = dalloc(&c->d_tq[0], B * bwt_squeue_per_block(c->S)))) return r;
         if ((r = dalloc(&c->d_tq[1], B * bwt_squeue_per_block(c->S)))) return r;
         if ((r = dalloc(&c->d_tc, 2 * B))) return r;
+        if ((r = dalloc(&c->d_lspill, B * c->stride))) return r;
         c->bwtq_blocks = (int)B;
     }
     const size_t Bs = ((size_t)c->bwtq_blocks + kBwtShards - 1) / kBwtShards;
@@ -272,7 +276,19 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
                        t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap, t.d_present);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");
+    static const bool wlevel = [] {
+        const char* e = getenv("BZ2MI_WLEVEL");
+        return !(e && *e == '0');
+    }();
     for (int d = 1; d <= kBwtLevels; ++d) {
+        if (wlevel && d < kBwtLevels) {
+            hipLaunchKernelGGL(bwt_wlevel_kernel, dim3(c->wlevel_grid), dim3(256), 0, s, t.d_blocks, c->stride,
+                               t.d_lens, t.d_sa, t.d_bwt, t.d_orig, c->d_lspill, c->d_lq[d & 1],
+                               lcount + d * kBwtShards, c->d_lq[(d + 1) & 1], lcount + (d + 1) * kBwtShards, lcap,
+                               c->d_sq, scount, scap, t.d_groups, t.d_ngroups, t.d_p2list, p2count);
+            HIPCHECK(hipGetLastError());
+            continue;
+        }
         hipLaunchKernelGGL(bwt_level_kernel, dim3(c->level_slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
                            t.d_sa, t.d_bwt, t.d_orig, c->d_lscratch, bwt_level_slot_bytes(c->S), c->S, c->d_lq[d & 1],
                            lcount + d * kBwtShards, c->d_lq[(d + 1) & 1], lcount + (d + 1) * kBwtShards, lcap,
@@ -675,6 +691,11 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
                                                          256, 0) != hipSuccess || occ < 1)
             occ = 4;
         c->level_slots = std::max(8, cus * occ / 8 * 8);
+        occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(bz2mi::bwt_wlevel_kernel),
+                                                         256, 0) != hipSuccess || occ < 1)
+            occ = 4;
+        c->wlevel_grid = std::max(8, cus * occ / 8 * 8);
     }
     if (dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S)) ||
         dalloc(&c->d_lscratch, c->level_slots * bz2mi::bwt_level_slot_bytes(c->S)) ||
@@ -706,7 +727,7 @@ void bz2mi_destroy(bz2mi_ctx* c) {
     for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB})
         if (st) (void)hipStreamSynchronize(st);
     std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_sq, c->d_lq[0], c->d_lq[1], c->d_tq[0], c->d_tq[1],
-                               c->d_tc, c->d_lscratch, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
+                               c->d_tc, c->d_lscratch, c->d_lspill, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
                                c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd,
                                c->d_starts, c->d_nb};
     for (const Batch& t : c->sets) {

@@ -892,15 +892,17 @@ __device__ __forceinline__ size_t shard_locate(const ShardIndex& si, uint32_t q,
 // d separates them).  Batches with no child of >= 2 rotations are dropped
 // (singletons are final).  Wave 0 packs with wave scans (4 children per
 // lane); returns the batch count (sh.bat_*).
-__device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
-    if (threadIdx.x < 64) {
+// One wave packs `hist`; w0 / w1 are 256-word scratch; returns the batch count.
+__device__ __forceinline__ uint32_t pack_children_wave(const uint32_t* hist, uint32_t* w0, uint32_t* w1,
+                                                       uint32_t* bat_start, uint32_t* bat_len) {
+    {
         const int lane = lane_id();
         constexpr uint32_t kHalf = kSmall / 2;
         uint32_t m[4], pos[4], sinc[4], brk[4];
         uint32_t tot = 0, stot = 0, btot = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            m[j] = sh.hist[lane * 4 + j];
+            m[j] = hist[lane * 4 + j];
             pos[j] = tot;
             tot += m[j];
             const bool small = m[j] > 0 && m[j] <= kHalf;
@@ -945,8 +947,8 @@ __device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
         // per batch: start, length, children, any child of >= 2
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            sh.wcnt[0][lane * 4 + j] = 0;  // length
-            sh.wcnt[1][lane * 4 + j] = 0;  // children | useful << 16
+            w0[lane * 4 + j] = 0;  // length
+            w1[lane * 4 + j] = 0;  // children | useful << 16
         }
         __builtin_amdgcn_wave_barrier();
         uint32_t idx = st_ex;
@@ -954,12 +956,12 @@ __device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
         for (int j = 0; j < 4; ++j) {
             const bool member = key[j] || (m[j] > kHalf && m[j] <= (uint32_t)kSmall);
             if (st[j]) {
-                sh.bat_start[idx] = pos_ex + pos[j];
+                bat_start[idx] = pos_ex + pos[j];
                 idx++;
             }
             if (member) {
-                atomicAdd(&sh.wcnt[0][idx - 1], m[j]);
-                atomicAdd(&sh.wcnt[1][idx - 1], 1u | (m[j] >= 2 ? 0x10000u : 0u));
+                atomicAdd(&w0[idx - 1], m[j]);
+                atomicAdd(&w1[idx - 1], 1u | (m[j] >= 2 ? 0x10000u : 0u));
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -968,10 +970,10 @@ __device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = (uint32_t)(lane * 4 + j);
-            const uint32_t ch = sh.wcnt[1][k];
+            const uint32_t ch = w1[k];
             keep[j] = k < nbat && (ch >> 16) != 0;
-            bs[j] = sh.bat_start[k];
-            bl[j] = sh.wcnt[0][k] | ((ch & 0xffffu) == 1 ? 0x80000000u : 0u);
+            bs[j] = bat_start[k];
+            bl[j] = w0[k] | ((ch & 0xffffu) == 1 ? 0x80000000u : 0u);
             nk += keep[j];
         }
         const uint32_t k_ex = wave_incl_sum(nk) - nk;
@@ -980,12 +982,20 @@ __device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (keep[j]) {
-                sh.bat_start[o] = bs[j];
-                sh.bat_len[o] = bl[j];
+                bat_start[o] = bs[j];
+                bat_len[o] = bl[j];
                 o++;
             }
         }
-        if (lane == 63) sh.cnt[7] = k_ex + nk;
+        __builtin_amdgcn_wave_barrier();
+        return (uint32_t)__builtin_amdgcn_readlane((int)(k_ex + nk), 63);
+    }
+}
+
+__device__ __forceinline__ uint32_t pack_children(BwtShared& sh) {
+    if (threadIdx.x < 64) {
+        const uint32_t nb = pack_children_wave(sh.hist, sh.wcnt[0], sh.wcnt[1], sh.bat_start, sh.bat_len);
+        if (threadIdx.x == 0) sh.cnt[7] = nb;
     }
     __syncthreads();
     return uniform(sh.cnt[7]);
@@ -1133,6 +1143,132 @@ struct LocalLarge {
     __device__ uint32_t reserve(uint32_t, uint32_t k) const { return atomicAdd(count, k); }
     __device__ void put(uint32_t, uint32_t slot, BwtItem it) const { q[slot] = Seg{it.start, it.len}; }
 };
+
+
+// Wave-level partition (levels before the last): one wave per segment, its
+// own LDS counters and stage, no workgroup barriers, so a workgroup works on
+// NW segments at once.  Segments longer than kWStage stage in `spill` (a
+// per-rotation array parallel to SA: segments never overlap).
+constexpr int kWStage = 1280;
+
+struct WaveLvl {
+    uint32_t hist[256];
+    uint32_t base[256];
+    uint32_t bat_start[256];
+    uint32_t bat_len[256];
+    uint32_t stage[kWStage];  // pack scratch after the scatter
+};
+
+struct WLevelLds {
+    ShardIndex si;
+    WaveLvl w[NW];
+};
+
+__device__ __forceinline__ void wave_sync_mem() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ void partition_segment_wave(const uint8_t* __restrict__ T, int n, uint32_t b, uint32_t* __restrict__ sa,
+                                       Seg seg, uint32_t d, WaveLvl& W, uint32_t* __restrict__ spill,
+                                       const Sharded<uint64_t>& sq, const Sharded<BwtItem>& lq,
+                                       const GroupSink& sink, uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig) {
+    const int lane = lane_id();
+    seg.start = uniform(seg.start);
+    seg.len = uniform(seg.len);
+    uint32_t* cp = seg.len <= (uint32_t)kWStage ? W.stage : spill + seg.start;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) W.hist[lane * 4 + j] = 0;
+    __builtin_amdgcn_wave_barrier();
+    constexpr int U = 8;
+    const uint32_t rounds = (seg.len + 63) / 64;
+    for (uint32_t r0 = 0; r0 < rounds; r0 += U) {
+        uint32_t iv[U], cv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t k = (r0 + j) * 64 + lane;
+            iv[j] = k < seg.len ? sa[seg.start + k] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t k = (r0 + j) * 64 + lane;
+            cv[j] = k < seg.len ? byte_at(T, n, iv[j] + d) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t k = (r0 + j) * 64 + lane;
+            const bool v = k < seg.len;
+            if (v) cp[k] = iv[j] | (cv[j] << 24);
+            const uint64_t peers = wave_match8(cv[j], v);
+            if (v && (peers & __lanemask_lt()) == 0) atomicAdd(&W.hist[cv[j]], (uint32_t)__popcll(peers));
+        }
+    }
+    wave_sync_mem();
+    // children: bytes 4*lane .. 4*lane+3
+    uint32_t c[4], ex[4], tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        c[j] = W.hist[lane * 4 + j];
+        ex[j] = tot;
+        tot += c[j];
+    }
+    const uint32_t lex = wave_incl_sum(tot) - tot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        ex[j] += lex;
+        W.base[lane * 4 + j] = ex[j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t k = r * 64 + lane;
+        const bool v = k < seg.len;
+        const uint32_t x = v ? cp[k] : 0u;
+        const uint32_t cc = x >> 24;
+        const uint64_t peers = wave_match8(cc, v);
+        const uint64_t below = peers & __lanemask_lt();
+        const int leader = peers ? __builtin_ctzll(peers) : 0;
+        uint32_t base = 0;
+        if (v && below == 0) base = atomicAdd(&W.base[cc], (uint32_t)__popcll(peers));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (v) sa[seg.start + base + (uint32_t)__popcll(below)] = x & 0xffffffu;
+    }
+    wave_sync_mem();  // stage reads done (pack scratch), SA scatter visible to the final reads
+    const uint32_t nbat = pack_children_wave(W.hist, W.stage, W.stage + 256, W.bat_start, W.bat_len);
+    bool large[4], deep[4];
+    uint32_t nl = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        deep[j] = c[j] > (uint32_t)kSmall && d + 1 >= (uint32_t)kMaxDepth;
+        large[j] = c[j] > (uint32_t)kSmall && !deep[j];
+        nl += large[j];
+    }
+    const uint32_t nl_ex = wave_incl_sum(nl) - nl;
+    const uint32_t nl_tot = (uint32_t)__builtin_amdgcn_readlane((int)(nl_ex + nl), 63);
+    uint32_t rs = 0, rl = 0;
+    if (lane == 0) {
+        rs = nbat ? sq.reserve(b, nbat) : 0u;
+        rl = nl_tot ? lq.reserve(b, nl_tot) : 0u;
+    }
+    rs = uniform(rs);
+    rl = uniform(rl) + nl_ex;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (c[j] == 1) {
+            const uint32_t i = sa[seg.start + ex[j]];
+            bwt[seg.start + ex[j]] = bwt_byte(T, n, i);
+            if (i == 0) *orig = seg.start + ex[j];
+        } else if (large[j]) {
+            lq.put(b, rl++, BwtItem{b, seg.start + ex[j], c[j], d + 1});
+        } else if (deep[j]) {
+            sink.push(Seg{seg.start + ex[j], c[j]});
+        }
+    }
+    for (uint32_t k = lane; k < nbat; k += 64) {
+        const uint32_t bl = W.bat_len[k];
+        sq.put(b, rs + k, sq_pack(b, seg.start + W.bat_start[k], bl & 0x7fffffffu, d + (bl >> 31)));
+    }
+    __builtin_amdgcn_wave_barrier();
+}
 
 }  // namespace
 
@@ -1282,6 +1418,40 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
     }
 #endif
     (void)item_t;
+}
+
+// ---- kernel 2w (levels before the last): one wave per large segment of the
+// level queue (wave-level partition, NW segments per workgroup at a time).
+// XCD split as in bwt_level_kernel.
+__global__ __launch_bounds__(256) void bwt_wlevel_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                         const uint32_t* __restrict__ lens,
+                                                         uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                         uint32_t* __restrict__ orig_out, uint32_t* __restrict__ spill_all,
+                                                         const BwtItem* __restrict__ lin,
+                                                         const uint32_t* __restrict__ lin_count,
+                                                         BwtItem* __restrict__ lout, uint32_t* __restrict__ lout_count,
+                                                         size_t lcap, uint64_t* __restrict__ squeue,
+                                                         uint32_t* __restrict__ scount, size_t scap,
+                                                         Seg* __restrict__ grp_all, uint32_t* __restrict__ ngroups,
+                                                         uint32_t* __restrict__ p2list, uint32_t* __restrict__ p2count) {
+    __shared__ WLevelLds L;
+    const uint32_t nin = shard_index_load(lin_count, L.si);
+    if (nin == 0) return;
+    const Sharded<uint64_t> sq{squeue, scount, scap};
+    const Sharded<BwtItem> lq{lout, lout_count, lcap};
+    WaveLvl& W = L.w[wave_id()];
+    const uint32_t xcd = blockIdx.x % kXcds, nloc = gridDim.x / kXcds;
+    const uint32_t qlo = (uint32_t)((uint64_t)nin * xcd / kXcds), qhi = (uint32_t)((uint64_t)nin * (xcd + 1) / kXcds);
+    for (uint32_t q = qlo + (blockIdx.x / kXcds) * NW + wave_id(); q < qhi; q += nloc * NW) {
+        const BwtItem it = lin[shard_locate(L.si, q, lcap)];
+        const uint32_t b = uniform(it.block);
+        const int n = (int)uniform(lens[b]);
+        const GroupSink sink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu, p2list,
+                             p2count, b, nullptr, nullptr};
+        partition_segment_wave(blocks + (size_t)b * stride, n, b, sa_all + (size_t)b * stride,
+                               Seg{it.start, it.len}, uniform(it.depth), W, spill_all + (size_t)b * stride, sq, lq,
+                               sink, bwt_out + (size_t)b * stride, orig_out + b);
+    }
 }
 
 // ---- kernel 3: one wave per queued batch of small segments (any block, any

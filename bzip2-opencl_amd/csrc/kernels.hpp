@@ -32,6 +32,11 @@ __global__ void bwt_level_kernel(const uint8_t* blocks, size_t stride, const uin
                                  int S, const BwtItem* lin, const uint32_t* lin_count, BwtItem* lout,
                                  uint32_t* lout_count, size_t lcap, uint64_t* squeue, uint32_t* scount, size_t scap,
                                  BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count, int last);
+__global__ void bwt_wlevel_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
+                                  uint8_t* bwt_out, uint32_t* orig_out, uint32_t* spill_all, const BwtItem* lin,
+                                  const uint32_t* lin_count, BwtItem* lout, uint32_t* lout_count, size_t lcap,
+                                  uint64_t* squeue, uint32_t* scount, size_t scap, BwtSeg* grp_all, uint32_t* ngroups,
+                                  uint32_t* p2list, uint32_t* p2count);
 __global__ void bwt_small_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                  uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* squeue,
                                  const uint32_t* scount, size_t scap, uint64_t* tl, uint32_t* tcount, size_t tcap);
