@@ -119,6 +119,7 @@ struct bz2mi_ctx {
     uint8_t* d_lscratch = nullptr;                  // their scratch slots
     int wlevel_grid = 0;                            // resident workgroups of bwt_wlevel_kernel
     uint32_t* d_lspill = nullptr;                   // wave-level stage spill (one word per rotation of a batch)
+    uint32_t* d_scb = nullptr;                      // per-block small-batch counts (LDS-text path)
     int bwtq_blocks = 0;           // capacity of the queues in blocks
     uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
     uint32_t* d_crctab = nullptr;
@@ -240,13 +241,14 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     if (nb > c->bwtq_blocks) {  // queues are shared by the batches: BWTs run one at a time
         HIPCHECK(hipStreamSynchronize(s));
         for (void* p : {(void*)c->d_sq, (void*)c->d_lq[0], (void*)c->d_lq[1], (void*)c->d_tq[0], (void*)c->d_tq[1],
-                        (void*)c->d_tc, (void*)c->d_lspill})
+                        (void*)c->d_tc, (void*)c->d_lspill, (void*)c->d_scb})
             if (p) (void)hipFree(p);
         c->d_sq = nullptr;
         c->d_lq[0] = c->d_lq[1] = nullptr;
         c->d_tq[0] = c->d_tq[1] = nullptr;
         c->d_tc = nullptr;
         c->d_lspill = nullptr;
+        c->d_scb = nullptr;
         c->bwtq_blocks = 0;
         const size_t B = (size_t)std::max(nb, 16);
         const size_t Bs = (B + kBwtShards - 1) / kBwtShards;  // blocks per shard
@@ -258,6 +260,7 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         if ((r = dalloc(&c->d_tq[1], B * bwt_squeue_per_block(c->S)))) return r;
         if ((r = dalloc(&c->d_tc, 2 * B))) return r;
         if ((r = dalloc(&c->d_lspill, B * c->stride))) return r;
+        if ((r = dalloc(&c->d_scb, B))) return r;
         c->bwtq_blocks = (int)B;
     }
     const size_t Bs = ((size_t)c->bwtq_blocks + kBwtShards - 1) / kBwtShards;
@@ -272,8 +275,26 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     uint32_t* tc[2] = {c->d_tc, c->d_tc + c->bwtq_blocks};
     uint32_t* p2count = t.d_bcnt + 768;
     uint32_t* pull = t.d_bcnt + 769;
-    hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
-                       t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap, t.d_present);
+    static const bool lds_text = [] {
+        const char* e = getenv("BZ2MI_LDSTEXT");
+        return !(e && *e == '0');
+    }();
+    // LDS-text path (blocks fit in LDS): the small batches of the levels go to
+    // per-block lists (counts d_scb, capacity tcap each) instead of the shards
+    const bool blk = lds_text && c->S <= kBwtLdsText;
+    uint32_t* sq_count = blk ? c->d_scb : scount;
+    const size_t sq_cap = blk ? tcap : scap;
+    const uint32_t smask = blk ? 0xffffffffu : (uint32_t)(kBwtShards - 1);
+    if (blk) {
+        HIPCHECK(hipMemsetAsync(c->d_scb, 0, nb * sizeof(uint32_t), s));
+        hipLaunchKernelGGL(bwt_block_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
+                           t.d_bwt, t.d_orig, c->d_lq[1], lcount + kBwtShards, lcap, t.d_present, c->d_tq[0], tc[0],
+                           tcap);
+    } else {
+        hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
+                           t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap,
+                           t.d_present);
+    }
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");
     static const bool wlevel = [] {
@@ -285,20 +306,24 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
             hipLaunchKernelGGL(bwt_wlevel_kernel, dim3(c->wlevel_grid), dim3(256), 0, s, t.d_blocks, c->stride,
                                t.d_lens, t.d_sa, t.d_bwt, t.d_orig, c->d_lspill, c->d_lq[d & 1],
                                lcount + d * kBwtShards, c->d_lq[(d + 1) & 1], lcount + (d + 1) * kBwtShards, lcap,
-                               c->d_sq, scount, scap, t.d_groups, t.d_ngroups, t.d_p2list, p2count);
+                               c->d_sq, sq_count, sq_cap, t.d_groups, t.d_ngroups, t.d_p2list, p2count, smask);
             HIPCHECK(hipGetLastError());
             continue;
         }
         hipLaunchKernelGGL(bwt_level_kernel, dim3(c->level_slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
                            t.d_sa, t.d_bwt, t.d_orig, c->d_lscratch, bwt_level_slot_bytes(c->S), c->S, c->d_lq[d & 1],
                            lcount + d * kBwtShards, c->d_lq[(d + 1) & 1], lcount + (d + 1) * kBwtShards, lcap,
-                           c->d_sq, scount, scap, t.d_groups, t.d_ngroups, t.d_p2list, p2count,
-                           d == kBwtLevels ? 1 : 0);
+                           c->d_sq, sq_count, sq_cap, t.d_groups, t.d_ngroups, t.d_p2list, p2count,
+                           d == kBwtLevels ? 1 : 0, smask);
         HIPCHECK(hipGetLastError());
     }
     STAGE_DONE("bwt_levels");
-    hipLaunchKernelGGL(bwt_small_kernel, dim3(c->small_grid), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
-                       t.d_sa, t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_tq[0], tc[0], tcap);
+    if (blk)
+        hipLaunchKernelGGL(bwt_block_small_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
+                           t.d_sa, t.d_bwt, t.d_orig, c->d_sq, c->d_scb, tcap, c->d_tq[0], tc[0], tcap);
+    else
+        hipLaunchKernelGGL(bwt_small_kernel, dim3(c->small_grid), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
+                           t.d_sa, t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_tq[0], tc[0], tcap);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_small");
     for (int r = 0; r < kBwtTieRounds; ++r) {
@@ -727,7 +752,7 @@ void bz2mi_destroy(bz2mi_ctx* c) {
     for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB})
         if (st) (void)hipStreamSynchronize(st);
     std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_sq, c->d_lq[0], c->d_lq[1], c->d_tq[0], c->d_tq[1],
-                               c->d_tc, c->d_lscratch, c->d_lspill, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
+                               c->d_tc, c->d_lscratch, c->d_lspill, c->d_scb, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
                                c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd,
                                c->d_starts, c->d_nb};
     for (const Batch& t : c->sets) {

@@ -662,43 +662,64 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
 constexpr int kSub = 32;
 
 struct Bucket2Lds {
+    static constexpr bool kKeys = true;
     uint32_t base[257];
     uint64_t key[kSmall];  // 8 bytes at depth d, grouped by byte d
     uint32_t idx[kSmall];  // rotation index | BWT byte << 24
 };
+// the same without the key copies, for a text held in LDS (keys re-read from it)
+struct Bucket3Lds {
+    static constexpr bool kKeys = false;
+    uint32_t base[257];
+    uint32_t idx[kSmall];
+};
+
+template <class BL>
+__device__ __forceinline__ uint64_t lds_key(const uint8_t* __restrict__ T, int n, const BL& L, uint32_t pos,
+                                            uint32_t d) {
+    if constexpr (BL::kKeys) {
+        return L.key[pos];
+    } else {
+        uint32_t p = (L.idx[pos] & 0xffffffu) + d;
+        if (p >= (uint32_t)n) p %= (uint32_t)n;
+        return load8(T, n, p);
+    }
+}
 
 // wave sort of LDS items [b0, b0+m) (m <= 64*E), emitted at seg.start + b0
-template <int E>
+template <int E, class BL>
 __device__ __forceinline__ void wave_sort_lds(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t start,
                                               uint32_t b0, uint32_t m, uint32_t d, const GroupSink& sink,
                                               uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
-                                              const Bucket2Lds& L) {
+                                              const BL& L) {
     const int lane = lane_id();
     uint64_t key[E];
     uint32_t lo[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t g = (uint32_t)(lane * E + e);
-        key[e] = g < m ? L.key[b0 + g] : ~0ull;
+        key[e] = g < m ? lds_key(T, n, L, b0 + g, d) : ~0ull;
         lo[e] = g < m ? L.idx[b0 + g] : ~0u;
     }
     wave_sort_emit<E, 0>(T, n, s, Seg{start + b0, m}, d, key, lo, sink, bwt, orig);
 }
 
+template <class BL>
 __device__ __forceinline__ void wave_sort_lds_any(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t start,
                                                uint32_t b0, uint32_t m, uint32_t d, const GroupSink& sink,
                                                uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
-                                               const Bucket2Lds& L) {
-    if (m <= 64) wave_sort_lds<1>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
-    else if (m <= 128) wave_sort_lds<2>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
-    else if (m <= 256) wave_sort_lds<4>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
-    else wave_sort_lds<8>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+                                               const BL& L) {
+    if (m <= 64) wave_sort_lds<1, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+    else if (m <= 128) wave_sort_lds<2, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+    else if (m <= 256) wave_sort_lds<4, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+    else wave_sort_lds<8, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
 }
 
 // `pre`: the batch's SA entries, loaded ahead by the caller (entry e*64+lane in pre[e])
+template <class BL>
 __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
                                   const GroupSink& sink, uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
-                                  Bucket2Lds& L, const uint32_t (&pre)[kSmall / 64]) {
+                                  BL& L, const uint32_t (&pre)[kSmall / 64]) {
     constexpr int E = kSmall / 64;
     const int lane = lane_id();
 #pragma unroll
@@ -739,7 +760,7 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
         for (int e = 0; e < E; ++e) {
             if ((uint32_t)(e * 64 + lane) < seg.len) {
                 const uint32_t pos = L.base[key[e] >> 56] + slot[e];
-                L.key[pos] = key[e];
+                if constexpr (BL::kKeys) L.key[pos] = key[e];
                 L.idx[pos] = ii[e];
             }
         }
@@ -762,7 +783,7 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
     for (int e = 0; e < E; ++e) {
         const uint32_t p = (uint32_t)(e * 64 + lane);
         const bool inseg = p < seg.len;
-        const uint64_t k = inseg ? L.key[p] : 0ull;
+        const uint64_t k = inseg ? lds_key(T, n, L, p, d) : 0ull;
         const uint32_t ii = inseg ? L.idx[p] : 0u;
         const uint32_t c = (uint32_t)(k >> 56);
         const uint32_t b0 = L.base[c], m = inseg ? L.base[c + 1] - b0 : 0u;
@@ -770,7 +791,7 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
         const uint32_t i = ii & 0xffffffu;
         uint32_t lt = 0, le = 0, eqlt = 0;
         for (uint32_t q = 0; q < (mine ? m : 0u); ++q) {
-            const uint64_t kq = L.key[b0 + q];
+            const uint64_t kq = lds_key(T, n, L, b0 + q, d);
             const uint32_t iq = L.idx[b0 + q] & 0xffffffu;
             lt += kq < k;
             le += kq <= k;
@@ -844,13 +865,14 @@ constexpr uint32_t kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin (
 template <typename Item>
 struct Sharded {
     Item* base;
-    uint32_t* counts;  // kShards counters
+    uint32_t* counts;  // kShards counters (mask ~0: one per block)
     size_t cap;        // entries per shard
+    uint32_t mask = kShards - 1;  // shard of block b = b & mask
     __device__ __forceinline__ uint32_t reserve(uint32_t b, uint32_t k) const {
-        return atomicAdd(&counts[b & (kShards - 1)], k);
+        return atomicAdd(&counts[b & mask], k);
     }
     __device__ __forceinline__ void put(uint32_t b, uint32_t slot, const Item& it) const {
-        base[(size_t)(b & (kShards - 1)) * cap + slot] = it;
+        base[(size_t)(b & mask) * cap + slot] = it;
     }
 };
 
@@ -1331,6 +1353,152 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
     if (large) lqs.put((uint32_t)b, sh.bcast[1] + rl, BwtItem{(uint32_t)b, ex, c, 1});
 }
 
+// ---- kernel 1' (blocks of <= kBwtLdsText bytes, replaces kernel 1 and the
+// small kernel's share of its batches): the block's text is copied into LDS
+// once (16-byte loads, the first-byte histogram on the way), the first-byte
+// counting sort is staged per 8192-rotation tile as in count_sort_first, and
+// then the workgroup's 16 waves sort the block's small batches themselves --
+// every 8-byte key and BWT byte is an LDS read instead of a gather from HBM
+// (the small kernel's text gathers missed L2 ~16x: 24 GB fetched per GiB).
+// Large buckets go to the level-1 queue as before.
+constexpr int FT = 1024;
+constexpr int FW = FT / 64;
+
+struct BlockLds {
+    uint4 text[kBwtLdsText / 16];
+    union {
+        uint32_t stage[FT * 8];
+        Bucket3Lds w[FW];
+    } u;
+    BwtShared sh;
+    uint32_t th[256], ts[256], tmp[FW];
+};
+
+__global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                       const uint32_t* __restrict__ lens, int nblocks,
+                                                       uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                       uint32_t* __restrict__ orig_out, BwtItem* __restrict__ lq,
+                                                       uint32_t* __restrict__ lcount, size_t lcap,
+                                                       uint32_t* __restrict__ present_out, uint64_t* __restrict__ tl,
+                                                       uint32_t* __restrict__ tcount, size_t tcap) {
+    __shared__ BlockLds L;
+    BwtShared& sh = L.sh;
+    const int b = blockIdx.x;
+    if (b >= nblocks) return;
+    const int t = threadIdx.x;
+    const int n = (int)uniform(lens[b]);
+    const uint8_t* T = blocks + (size_t)b * stride;
+    uint8_t* out = bwt_out + (size_t)b * stride;
+    if (n <= 1) {
+        if (t == 0) {
+            if (n == 1) out[0] = T[0];
+            orig_out[b] = 0;
+        }
+        if (t < 8) present_out[(size_t)b * 8 + t] = (n == 1 && (T[0] >> 5) == t) ? 1u << (T[0] & 31) : 0u;
+        return;
+    }
+    uint32_t* sa = sa_all + (size_t)b * stride;
+    const uint8_t* Tl = reinterpret_cast<const uint8_t*>(L.text);
+    // ---- text -> LDS (whole 16-byte chunks: the block buffer is padded),
+    // first-byte histogram
+    if (t < 256) sh.hist[t] = 0;
+    __syncthreads();
+    {
+        const int n16 = (n + 15) >> 4;
+        const uint4* T4 = reinterpret_cast<const uint4*>(T);
+        for (int v = t; v < n16; v += FT) {
+            const uint4 w = T4[v];
+            L.text[v] = w;
+            const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+            const int lim = n - v * 16;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < lim) atomicAdd(&sh.hist[(ww[k >> 2] >> ((k & 3) * 8)) & 255u], 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t c = t < 256 ? sh.hist[t] : 0u;
+    uint32_t total;
+    const uint32_t ex = wg_excl_sum<FT>(c, L.tmp, &total);
+    if (t < 256) sh.base[t] = ex;
+    // ---- first-byte scatter, one 8192-rotation tile at a time (8 per thread)
+    for (int tile0 = 0; tile0 < n; tile0 += FT * 8) {
+        if (t < 256) L.th[t] = 0;
+        __syncthreads();
+        const int i0 = tile0 + t * 8;
+        uint32_t bv[8], rk[8];
+        {
+            const uint2 w = i0 < n ? reinterpret_cast<const uint2*>(Tl)[i0 >> 3] : make_uint2(0u, 0u);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) bv[k] = ((k < 4 ? w.x : w.y) >> ((k & 3) * 8)) & 255u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rk[k] = i0 + k < n ? atomicAdd(&L.th[bv[k]], 1u) : 0u;
+        __syncthreads();
+        uint32_t tn;
+        const uint32_t tsv = wg_excl_sum<FT>(t < 256 ? L.th[t] : 0u, L.tmp, &tn);
+        if (t < 256) L.ts[t] = tsv;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (i0 + k < n) L.u.stage[L.ts[bv[k]] + rk[k]] = (uint32_t)(i0 + k) | (bv[k] << 24);
+        __syncthreads();
+        for (uint32_t j = t; j < tn; j += FT) {
+            const uint32_t v = L.u.stage[j], b8 = v >> 24;
+            sa[sh.base[b8] + (j - L.ts[b8])] = v & 0xffffffu;
+        }
+        __syncthreads();
+        if (t < 256) sh.base[t] += L.th[t];
+    }
+    __syncthreads();
+    if (t < 256) {  // symbols in use (the MTF symbol map): bit t of the 256-bit set
+        const uint64_t m = __ballot(c != 0);
+        if (lane_id() == 0) {
+            present_out[(size_t)b * 8 + 2 * wave_id()] = (uint32_t)m;
+            present_out[(size_t)b * 8 + 2 * wave_id() + 1] = (uint32_t)(m >> 32);
+        }
+        if (c == 1) {
+            const uint32_t i = sa[ex];
+            out[ex] = bwt_byte(Tl, n, i);
+            if (i == 0) orig_out[b] = ex;
+        }
+    }
+    const Sharded<BwtItem> lqs{lq, lcount, lcap};
+    const uint32_t nbat = pack_children(sh);
+    const bool large = t < 256 && c > (uint32_t)kSmall;
+    uint32_t nl;
+    const uint32_t rl = wg_excl_sum<FT>(large ? 1u : 0u, L.tmp, &nl);
+    if (t == 0) sh.bcast[1] = nl ? lqs.reserve((uint32_t)b, nl) : 0u;
+    __syncthreads();
+    if (large) lqs.put((uint32_t)b, sh.bcast[1] + rl, BwtItem{(uint32_t)b, ex, c, 1});
+    // ---- the small batches, one wave each, keys from the LDS text; the next
+    // batch's SA entries are loaded while the current one is sorted
+    constexpr int E = kSmall / 64;
+    const int w = wave_id(), lane = lane_id();
+    Scratch s{};
+    s.sa = sa;
+    const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, (uint32_t)b, tl + (size_t)b * tcap, tcount + b};
+    auto load_batch = [&](uint32_t k, uint32_t (&pre)[E]) {
+        const uint32_t st = sh.bat_start[k], len = sh.bat_len[k] & 0x7fffffffu;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t g = (uint32_t)(e * 64 + lane);
+            pre[e] = g < len ? sa[st + g] : 0u;
+        }
+    };
+    uint32_t cur[E];
+    if ((uint32_t)w < nbat) load_batch((uint32_t)w, cur);
+    for (uint32_t k = (uint32_t)w; k < nbat; k += FW) {
+        uint32_t nxt[E];
+        if (k + FW < nbat) load_batch(k + FW, nxt);
+        const uint32_t bl = uniform(sh.bat_len[k]);
+        const Seg seg{uniform(sh.bat_start[k]), bl & 0x7fffffffu};
+        wave_sort_bucket2(Tl, n, s, seg, bl >> 31, sink, out, orig_out + b, L.u.w[w], cur);
+#pragma unroll
+        for (int e = 0; e < E; ++e) cur[e] = nxt[e];
+    }
+}
+
 // ---- kernel 2 (one launch per level, all blocks at once): every large
 // segment of the level queue is partitioned by one workgroup.  The last level
 // (`last` != 0) keeps partitioning its segment's large children itself, level
@@ -1345,7 +1513,7 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
                                                         uint64_t* __restrict__ squeue, uint32_t* __restrict__ scount,
                                                         size_t scap, Seg* __restrict__ grp_all,
                                                         uint32_t* __restrict__ ngroups, uint32_t* __restrict__ p2list,
-                                                        uint32_t* __restrict__ p2count, int last) {
+                                                        uint32_t* __restrict__ p2count, int last, uint32_t smask) {
     __shared__ LevelLds L;
     const uint32_t nin = shard_index_load(lin_count, L.si);
     if (nin == 0) return;
@@ -1360,7 +1528,7 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
         s.large2 = (Seg*)p;
     }
     const int t = threadIdx.x;
-    const Sharded<uint64_t> sq{squeue, scount, scap};
+    const Sharded<uint64_t> sq{squeue, scount, scap, smask};
     PartTimes pt{};
     unsigned long long item_t = 0;
     // XCD-aware: workgroups are dealt to the 8 XCDs round-robin; XCD x takes
@@ -1433,11 +1601,12 @@ __global__ __launch_bounds__(256) void bwt_wlevel_kernel(const uint8_t* __restri
                                                          size_t lcap, uint64_t* __restrict__ squeue,
                                                          uint32_t* __restrict__ scount, size_t scap,
                                                          Seg* __restrict__ grp_all, uint32_t* __restrict__ ngroups,
-                                                         uint32_t* __restrict__ p2list, uint32_t* __restrict__ p2count) {
+                                                         uint32_t* __restrict__ p2list, uint32_t* __restrict__ p2count,
+                                                         uint32_t smask) {
     __shared__ WLevelLds L;
     const uint32_t nin = shard_index_load(lin_count, L.si);
     if (nin == 0) return;
-    const Sharded<uint64_t> sq{squeue, scount, scap};
+    const Sharded<uint64_t> sq{squeue, scount, scap, smask};
     const Sharded<BwtItem> lq{lout, lout_count, lcap};
     WaveLvl& W = L.w[wave_id()];
     const uint32_t xcd = blockIdx.x % kXcds, nloc = gridDim.x / kXcds;
@@ -1510,6 +1679,68 @@ __global__ __launch_bounds__(256, 4) void bwt_small_kernel(const uint8_t* __rest
         nc = nn;
         ec = en;
         en = enn;
+    }
+}
+
+// ---- kernel 3' (with kernel 1'): the batches the levels queued, per block
+// (one list per block), sorted by one 1024-thread workgroup per block with
+// the block's text in LDS; blocks with an empty list return at once.
+struct BlockSmallLds {
+    uint4 text[kBwtLdsText / 16];
+    Bucket3Lds w[FW];
+};
+
+__global__ __launch_bounds__(FT) void bwt_block_small_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                             const uint32_t* __restrict__ lens, int nblocks,
+                                                             uint32_t* __restrict__ sa_all,
+                                                             uint8_t* __restrict__ bwt_out,
+                                                             uint32_t* __restrict__ orig_out,
+                                                             const uint64_t* __restrict__ squeue,
+                                                             const uint32_t* __restrict__ scount, size_t scap,
+                                                             uint64_t* __restrict__ tl, uint32_t* __restrict__ tcount,
+                                                             size_t tcap) {
+    __shared__ BlockSmallLds L;
+    const int b = blockIdx.x;
+    if (b >= nblocks) return;
+    const uint32_t nq = uniform(scount[b]);
+    if (nq == 0) return;
+    const int t = threadIdx.x;
+    const int n = (int)uniform(lens[b]);
+    {
+        const int n16 = (n + 15) >> 4;
+        const uint4* T4 = reinterpret_cast<const uint4*>(blocks + (size_t)b * stride);
+        for (int v = t; v < n16; v += FT) L.text[v] = T4[v];
+    }
+    __syncthreads();
+    const uint8_t* Tl = reinterpret_cast<const uint8_t*>(L.text);
+    uint32_t* sa = sa_all + (size_t)b * stride;
+    uint8_t* out = bwt_out + (size_t)b * stride;
+    const uint64_t* q = squeue + (size_t)b * scap;
+    constexpr int E = kSmall / 64;
+    const int w = wave_id(), lane = lane_id();
+    Scratch s{};
+    s.sa = sa;
+    const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, (uint32_t)b, tl + (size_t)b * tcap, tcount + b};
+    auto load_batch = [&](uint64_t e, uint32_t (&pre)[E]) {
+        const uint32_t st = uniform((uint32_t)(e >> 22) & 0xfffffu), len = uniform((uint32_t)(e >> 13) & 511u) + 1u;
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            const uint32_t g = (uint32_t)(k * 64 + lane);
+            pre[k] = g < len ? sa[st + g] : 0u;
+        }
+    };
+    uint32_t cur[E];
+    uint64_t ec = (uint32_t)w < nq ? q[w] : 0ull;
+    if ((uint32_t)w < nq) load_batch(ec, cur);
+    for (uint32_t k = (uint32_t)w; k < nq; k += FW) {
+        uint32_t nxt[E];
+        const uint64_t en = k + FW < nq ? q[k + FW] : 0ull;
+        if (k + FW < nq) load_batch(en, nxt);
+        const Seg seg{uniform((uint32_t)(ec >> 22) & 0xfffffu), uniform((uint32_t)(ec >> 13) & 511u) + 1u};
+        wave_sort_bucket2(Tl, n, s, seg, uniform((uint32_t)ec & 0x1fffu), sink, out, orig_out + b, L.w[w], cur);
+#pragma unroll
+        for (int e = 0; e < E; ++e) cur[e] = nxt[e];
+        ec = en;
     }
 }
 

@@ -27,16 +27,31 @@ __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const ui
                                   uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint64_t* squeue,
                                   uint32_t* scount, size_t scap, BwtItem* lq, uint32_t* lcount, size_t lcap,
                                   uint32_t* present_out);
+// Blocks of <= kBwtLdsText bytes: the first-byte sort and the sort of the
+// small buckets in one launch, the block's text held in LDS (1024 threads, one
+// workgroup per CU).  Large buckets still go to the level queue.
+constexpr int kBwtLdsText = 90112;
+__global__ void bwt_block_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
+                                 uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, BwtItem* lq,
+                                 uint32_t* lcount, size_t lcap, uint32_t* present_out, uint64_t* tl,
+                                 uint32_t* tcount, size_t tcap);
 __global__ void bwt_level_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                  uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,
                                  int S, const BwtItem* lin, const uint32_t* lin_count, BwtItem* lout,
                                  uint32_t* lout_count, size_t lcap, uint64_t* squeue, uint32_t* scount, size_t scap,
-                                 BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count, int last);
+                                 BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count, int last,
+                                 uint32_t smask);
 __global__ void bwt_wlevel_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                   uint8_t* bwt_out, uint32_t* orig_out, uint32_t* spill_all, const BwtItem* lin,
                                   const uint32_t* lin_count, BwtItem* lout, uint32_t* lout_count, size_t lcap,
                                   uint64_t* squeue, uint32_t* scount, size_t scap, BwtSeg* grp_all, uint32_t* ngroups,
-                                  uint32_t* p2list, uint32_t* p2count);
+                                  uint32_t* p2list, uint32_t* p2count, uint32_t smask);
+// with bwt_block_kernel: the levels' small batches in per-block lists (squeue
+// + b * scap, count scount[b]), one workgroup per block, text in LDS
+__global__ void bwt_block_small_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
+                                       uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* squeue,
+                                       const uint32_t* scount, size_t scap, uint64_t* tl, uint32_t* tcount,
+                                       size_t tcap);
 __global__ void bwt_small_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                  uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* squeue,
                                  const uint32_t* scount, size_t scap, uint64_t* tl, uint32_t* tcount, size_t tcap);
