@@ -362,7 +362,8 @@ int stage_seed(bz2mi_ctx* c, Batch& t, int nb, uint64_t first_block, hipStream_t
 
 int stage_huffman(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     using namespace bz2mi;
-    hipLaunchKernelGGL(huffman_kernel, dim3(nb), dim3(256), 0, s, t.d_mtf, c->mtf_stride, t.d_mtflen, t.d_alpha,
+    const size_t sel_bytes = ((size_t)(c->S + 1 + 49) / 50 + 15) & ~(size_t)15;
+    hipLaunchKernelGGL(huffman_kernel, dim3(nb), dim3(256), sel_bytes, s, t.d_mtf, c->mtf_stride, t.d_mtflen, t.d_alpha,
                        t.d_seed, t.d_present, t.d_orig, nb, t.d_payload, c->payload_words, t.d_pbits);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("huffman");

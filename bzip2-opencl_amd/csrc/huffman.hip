@@ -35,14 +35,12 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int NW = NT / 64;
-constexpr int kMaxSel = 18432;                       // >= ceil(900001/50): 900 KB block mode
 constexpr int kTileSyms = 8 * NT;                    // symbols per data tile
 constexpr int kWinWords = kTileSyms * kMaxCodeLen / 32 + 2;
 
 struct HufShared {
     uint8_t lens[kMaxTables][kMaxAlpha + 2];
     uint64_t pack[kMaxAlpha];
-    uint8_t sel[kMaxSel];
     union {
         struct {
             int tf[kMaxTables][kMaxAlpha];
@@ -385,12 +383,20 @@ int huffman_phases(unsigned long long* out) {
 #endif
 }
 
-__global__ __launch_bounds__(256) void huffman_kernel(
+// 6 workgroups per CU: the length builds are serial, latency-bound wave code,
+// so more resident blocks pay for a few spilled registers
+#ifndef BZ2MI_HUF_WGS
+#define BZ2MI_HUF_WGS 6
+#endif
+__global__ __launch_bounds__(256, BZ2MI_HUF_WGS) void huffman_kernel(
     const uint16_t* __restrict__ mtf, size_t mtf_stride, const uint32_t* __restrict__ mtf_len,
     const uint32_t* __restrict__ alpha_in, const uint32_t* __restrict__ seed,
     const uint32_t* __restrict__ present, const uint32_t* __restrict__ orig, int nblocks,
     uint32_t* __restrict__ payload, size_t payload_words, uint64_t* __restrict__ payload_bits) {
     __shared__ HufShared sh;
+    // selectors: dynamic LDS sized by the launcher for its block size
+    // (ceil((S + 1) / 50) bytes: 1.8 KB at S = 90,000, 18 KB at 900,000)
+    extern __shared__ uint8_t sel[];
     const int b = blockIdx.x;
     if (b >= nblocks) return;
     const int t = threadIdx.x, lane = lane_id();
@@ -454,7 +460,7 @@ __global__ __launch_bounds__(256) void huffman_kernel(
 #pragma unroll
                 for (int k = 0; k < kGroupRun / 2; ++k) c += sh.pack[w[k] & 0xffffu] + sh.pack[w[k] >> 16];
                 const int best = best_table(c, T);
-                sh.sel[g] = (uint8_t)best;
+                sel[g] = (uint8_t)best;
                 int* tf = sh.u.opt.tf[best];
 #pragma unroll
                 for (int k = 0; k < kGroupRun / 2; ++k) {
@@ -465,7 +471,7 @@ __global__ __launch_bounds__(256) void huffman_kernel(
                 uint64_t c = 0;
                 for (int i = g0; i < m; ++i) c += sh.pack[X[i]];
                 const int best = best_table(c, T);
-                sh.sel[g] = (uint8_t)best;
+                sel[g] = (uint8_t)best;
                 for (int i = g0; i < m; ++i) atomicAdd(&sh.u.opt.tf[best][X[i]], 1);
             }
         }
@@ -523,7 +529,7 @@ __global__ __launch_bounds__(256) void huffman_kernel(
     int last0[kMaxTables];
 #pragma unroll
     for (int u = 0; u < kMaxTables; ++u) last0[u] = -1;
-    for (int g = s0; g < s1; ++g) note_use(last0, sh.sel[g], g);
+    for (int g = s0; g < s1; ++g) note_use(last0, sel[g], g);
     wg_excl_max6(last0, sh);  // (its barriers also complete the codes)
     uint32_t mysel = 0;
     {
@@ -531,7 +537,7 @@ __global__ __launch_bounds__(256) void huffman_kernel(
 #pragma unroll
         for (int u = 0; u < kMaxTables; ++u) last[u] = last0[u];
         for (int g = s0; g < s1; ++g) {
-            const int v = sh.sel[g];
+            const int v = sel[g];
             mysel += (uint32_t)selector_pos(last, v) + 1u;
             note_use(last, v, g);
         }
@@ -580,7 +586,7 @@ __global__ __launch_bounds__(256) void huffman_kernel(
 #pragma unroll
         for (int u = 0; u < kMaxTables; ++u) last[u] = last0[u];
         for (int g = s0; g < s1; ++g) {
-            const int v = sh.sel[g];
+            const int v = sel[g];
             const int pos = selector_pos(last, v);
             s.put(pos + 1, ((1u << pos) - 1u) << 1);
             note_use(last, v, g);
@@ -647,7 +653,7 @@ __global__ __launch_bounds__(256) void huffman_kernel(
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int i = i0 + k;
-            cs[k] = i < m ? sh.u.out.codes[sh.sel[(unsigned)i / kGroupRun]][sym[k]] : 0u;
+            cs[k] = i < m ? sh.u.out.codes[sel[(unsigned)i / kGroupRun]][sym[k]] : 0u;
             mybits += cs[k] >> 24;
         }
         uint32_t tilebits;
