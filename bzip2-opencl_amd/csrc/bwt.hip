@@ -652,7 +652,7 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
 // ---- a bucket of <= 512 rotations with a common prefix of d bytes, on one
 // wave.  The 8-byte keys at depth d are loaded once and counting-sorted by
 // their first byte (byte d) into LDS sub-buckets.  Then either
-//   * text-like segments (most rotations in sub-buckets of > kSub): one wave
+//   * text-like segments (>= 1/8 of the rotations in sub-buckets of > kSub): one wave
 //     sort of the whole segment on the keys, or
 //   * every rotation of a sub-bucket of <= kSub finds its place by counting
 //     the smaller (key, index) pairs of its sub-bucket (wide alphabets: one
@@ -774,7 +774,9 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
         inbig += m > (uint32_t)kSub ? m : 0u;
     }
     const uint32_t nbig = wave_sum(inbig);
-    if (2 * nbig > seg.len) {
+    // (a whole-segment sort unless fewer than 1/8 of the rotations are in big
+    // sub-buckets: measured on text, 2 -> 8 saves ~1% of the BWT)
+    if (8 * nbig > seg.len) {
         wave_sort_lds_any(T, n, s, seg.start, 0, seg.len, d, sink, bwt, orig, L);
         return;
     }
