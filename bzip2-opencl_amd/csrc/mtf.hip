@@ -17,6 +17,8 @@
 // :2565-2572).  Zero ranks are coded as bijective base-2 RUNA/RUNB digits
 // (:2585-2606); the per-block histogram of the emitted symbols (258 bins) is
 // what the reference adds into its frequency array (:2613, :2641-2643).
+#include <type_traits>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -125,6 +127,10 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
         return at < n ? *reinterpret_cast<const uint4*>(X + at) : make_uint4(0, 0, 0, 0);
     };
     uint4 cur = load16(16 * j);
+    // the tile loop, instantiated for the words of the 256-bit symbol sets
+    // the block's k symbols occupy (2, 4 or 8): fewer OR-scans per tile
+    auto tiles = [&](auto kw) {
+    constexpr int KW = decltype(kw)::value;
     for (int sb = 0; sb < n; sb += kSuper) {
         __syncthreads();  // the previous superblock is consumed
         *reinterpret_cast<uint4*>(sh.sym + 16 * j) = cur;
@@ -153,22 +159,26 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
             // ---- first in the tile: |T_j| + R0 - #{c in T_j : R0(c) < R0}
             const uint64_t FO = __ballot(fo);
             const uint32_t w = R0 >> 5, bit = 1u << (R0 & 31);
-            uint32_t qi[8];
+            // the scans of the 256-bit first-occurrence sets: only the KW words
+            // the block's k symbols can occupy (list positions < k)
+            uint32_t qall[8];
             uint32_t less = 0;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                qi[e] = wave_incl_or((fo && w == (uint32_t)e) ? bit : 0u);
-                const uint32_t m = (uint32_t)e < w ? ~0u : ((uint32_t)e == w ? bit - 1 : 0u);
-                less += (uint32_t)__popc(qi[e] & m);
+                if (e < KW) {
+                    const uint32_t qv = wave_incl_or((fo && w == (uint32_t)e) ? bit : 0u);
+                    const uint32_t m = (uint32_t)e < w ? ~0u : ((uint32_t)e == w ? bit - 1 : 0u);
+                    less += (uint32_t)__popc(qv & m);
+                    qall[e] = (uint32_t)__builtin_amdgcn_readlane((int)qv, 63);
+                } else {
+                    qall[e] = 0u;
+                }
             }
             const uint32_t rB = (uint32_t)__popcll(FO & below) + R0 - less;
             const uint32_t rank = hasprv ? rC : rB;
             // ---- list of the next tile
             const uint64_t LO = ~readlane64(Pinc, 63) & lmask;  // last occurrences
             const uint32_t D = (uint32_t)__popcll(LO);
-            uint32_t qall[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) qall[e] = (uint32_t)__builtin_amdgcn_readlane((int)qi[e], 63);
             {
                 const uint32_t lw = reinterpret_cast<const uint32_t*>(sh.lst)[j];  // positions 4j..4j+3
                 uint32_t qa = 0, cb = 0;
@@ -216,6 +226,10 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
             carry = NZ ? (uint32_t)(nlive - 1 - msb64(NZ)) : carry + (uint32_t)nlive;
         }
     }
+    };
+    if (k <= 64) tiles(std::integral_constant<int, 2>{});
+    else if (k <= 128) tiles(std::integral_constant<int, 4>{});
+    else tiles(std::integral_constant<int, 8>{});
     if (carry) {  // the block ends in a zero run
         if (j == 0) emit_run(carry, out, o, na, nb);
         o += run_ndigits(carry);
