@@ -161,17 +161,15 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
             const uint32_t w = R0 >> 5, bit = 1u << (R0 & 31);
             // the scans of the 256-bit first-occurrence sets: only the KW words
             // the block's k symbols can occupy (list positions < k)
-            uint32_t qall[8];
+            uint32_t qi[8], qall[8];
             uint32_t less = 0;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
+                qi[e] = 0u;
                 if (e < KW) {
-                    const uint32_t qv = wave_incl_or((fo && w == (uint32_t)e) ? bit : 0u);
+                    qi[e] = wave_incl_or((fo && w == (uint32_t)e) ? bit : 0u);
                     const uint32_t m = (uint32_t)e < w ? ~0u : ((uint32_t)e == w ? bit - 1 : 0u);
-                    less += (uint32_t)__popc(qv & m);
-                    qall[e] = (uint32_t)__builtin_amdgcn_readlane((int)qv, 63);
-                } else {
-                    qall[e] = 0u;
+                    less += (uint32_t)__popc(qi[e] & m);
                 }
             }
             const uint32_t rB = (uint32_t)__popcll(FO & below) + R0 - less;
@@ -179,6 +177,8 @@ __global__ __launch_bounds__(64) void mtf_kernel(const uint8_t* __restrict__ bwt
             // ---- list of the next tile
             const uint64_t LO = ~readlane64(Pinc, 63) & lmask;  // last occurrences
             const uint32_t D = (uint32_t)__popcll(LO);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) qall[e] = e < KW ? (uint32_t)__builtin_amdgcn_readlane((int)qi[e], 63) : 0u;
             {
                 const uint32_t lw = reinterpret_cast<const uint32_t*>(sh.lst)[j];  // positions 4j..4j+3
                 uint32_t qa = 0, cb = 0;
