@@ -6,9 +6,12 @@ bytes resident in HBM, compressed at -9 with the reference's block size
 (S = 9 x 10,000 = 90,000 bytes, Config.hpp:30) and parallel count p = 10, to a
 complete .bz2 stream in HBM.  One step = one whole stream: device RLE1 front
 end + block split + CRCs, BWT, MTF/RLE2, seed carry-over, Huffman + packing,
-stream assembly.  Multi-GPU (torchrun, one process per GPU): every rank
-compresses its own 1 GiB object (independent .bz2 streams, no data-path
-collective) -> weak scaling; timing is the max over ranks.
+stream assembly.  Multi-GPU (--gpus N: one process per GPU, self-launched
+through torch.distributed.run when not started by it): ONE logical stream of
+N x 1 GiB, cut into units interleaved over the ranks, compressed with the unit
+protocol of bz2mi.shard (chain token, seed-sum all-gather, bit-offset scan;
+SURVEY.md section 8(e)) into the same bytes one device would write -> weak
+scaling; timing is the max over ranks.
 
 Prints ONE JSON line (rank 0) with the contract fields plus `roofline` (the
 dominant kernel against the HBM roofline) and `cpu_baseline` (the reference
@@ -66,15 +69,38 @@ def stage_traffic(args, stage):
         return None, None
 
 
+def host_cpu() -> dict:
+    """Host CPU model and the cores this process may use (the GPU box gives a
+    1-GPU job a share of the machine: os.sched_getaffinity, at most 16)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return {"model": model, "cores_available": avail, "cores_used_parallel": max(1, min(16, avail))}
+
+
 def cpu_baseline(sample_bytes: int) -> dict:
     """Reference compressor (O_ref = the reference's own kernel.cpp + host code,
     oracle/_ref/liboref.so) or, where it was not built, the C restatement
-    cpu_ref; one thread, bounded sample of the same workload."""
-    import numpy as np
+    cpu_ref; one thread, bounded sample of the same workload.  Context in the
+    same run: cpu_ref on all usable cores (block-parallel, bit-identical output)
+    and libbz2 1.0.8 at -9 (bzip2's own 900 KB blocks, different bytes)."""
+    import bz2
     from bz2mi import synth
     data = synth.random_bytes(sample_bytes).tobytes()
     oref = os.path.join(REPO, "oracle", "_ref", "liboref.so")
     cref = os.path.join(REPO, "oracle", "_build", "libcpuref.so")
+    cpu = host_cpu()
+    res = None
     if os.path.exists(oref):
         L = ctypes.CDLL(oref)
         L.oref_compress.restype = ctypes.c_longlong
@@ -85,26 +111,42 @@ def cpu_baseline(sample_bytes: int) -> dict:
         t0 = time.perf_counter()
         n = L.oref_compress(data, len(data), 9, 10, 10000, out, cap)
         dt = time.perf_counter() - t0
-        kind = "reference"
-        label = "O_ref (reference kernel.cpp + BlockCompressor/BitOutputStream compiled for the host, serial)"
-    elif os.path.exists(cref):
+        if n >= 0:
+            res = {"value": round(len(data) / dt / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "reference",
+                   "sample": f"{len(data) >> 20} MiB of the same random-byte workload at -9, p=10, one thread: "
+                             "O_ref (reference kernel.cpp + BlockCompressor/BitOutputStream compiled for the host, "
+                             "serial)", "seconds": round(dt, 2)}
+    if os.path.exists(cref):
         L = ctypes.CDLL(cref)
         L.cpuref_compress.restype = ctypes.c_longlong
         L.cpuref_bound.restype = ctypes.c_size_t
         cap = L.cpuref_bound(ctypes.c_size_t(len(data)), 9, 10000)
         out = ctypes.create_string_buffer(cap)
+        if res is None:
+            t0 = time.perf_counter()
+            n = L.cpuref_compress(data, ctypes.c_size_t(len(data)), 9, 10, 10000, out, ctypes.c_size_t(cap), 1)
+            dt = time.perf_counter() - t0
+            if n >= 0:
+                res = {"value": round(len(data) / dt / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+                       "sample": f"{len(data) >> 20} MiB of the same random-byte workload at -9, p=10, one "
+                                 "thread: cpu_ref (oracle/cpu_ref.c restatement)", "seconds": round(dt, 2)}
+        th = cpu["cores_used_parallel"]
         t0 = time.perf_counter()
-        n = L.cpuref_compress(data, ctypes.c_size_t(len(data)), 9, 10, 10000, out, ctypes.c_size_t(cap), 1)
+        n = L.cpuref_compress(data, ctypes.c_size_t(len(data)), 9, 10, 10000, out, ctypes.c_size_t(cap), th)
         dt = time.perf_counter() - t0
-        kind = "port"
-        label = "cpu_ref (oracle/cpu_ref.c restatement)"
-    else:
+        if res is not None and n >= 0:
+            res["all_cores"] = {"value": round(len(data) / dt / 1e6, 3), "unit": "MB/s", "threads": th,
+                                "what": "cpu_ref block-parallel on a pthread pool, same bytes as O_ref"}
+    if res is None:
         return None
-    if n < 0:
-        return None
-    return {"value": round(len(data) / dt / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": kind,
-            "sample": f"{len(data) >> 20} MiB of the same random-byte workload at -9, p=10, one thread: {label}",
-            "seconds": round(dt, 2)}
+    sub = data[: min(len(data), 32 << 20)]
+    t0 = time.perf_counter()
+    bz2.compress(sub, 9)
+    dt = time.perf_counter() - t0
+    res["bzip2_9"] = {"value": round(len(sub) / dt / 1e6, 3), "unit": "MB/s", "threads": 1,
+                      "what": f"libbz2 1.0.8 -9 (900 KB blocks) on {len(sub) >> 20} MiB of the sample (context only)"}
+    res["host_cpu"] = cpu
+    return res
 
 
 def main():
@@ -125,19 +167,34 @@ def main():
     ap.add_argument("--data", choices=["random", "text", "mixed"], default="random",
                     help="random = C2 (the bench line); text = C3 stand-in (seeded word Markov text, enwik9 is "
                          "not available offline); mixed = C4 (rotating random/text/runs/ACGT segments)")
+    ap.add_argument("--units-per-gpu", type=int, default=4,
+                    help="N > 1: units of the logical stream per rank (interleaved over the ranks)")
+    ap.add_argument("--gather", choices=["none", "rank0"], default="none",
+                    help="N > 1: rank0 = also gather the stream onto rank 0 over RCCL inside the timed step; "
+                         "none = the stream ends distributed (each rank holds its units' final bytes), the "
+                         "gather is then timed once after the steps and reported beside the line")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: relaunch under torch.distributed.run before any GPU call
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        return bench_units(args, world)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+    torch.cuda.set_device(local)
     ensure_built()
     import bz2mi
 
@@ -240,6 +297,160 @@ def main():
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def unit_bytes(args, g: int, U: int, dev):
+    """Unit g of the logical stream (U bytes) on `dev`: random = torch Philox
+    with seed 0x5EED0001 + g; text = word-Markov text with seed 0x5EED0002 + g;
+    mixed = the C4 stream of 64 MiB segments (unit g = segments g*U/64Mi ...)."""
+    import torch
+    from bz2mi import synth
+    if args.data == "random":
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(synth.SEED_RANDOM + g)
+        return torch.randint(0, 256, (U,), dtype=torch.uint8, device=dev, generator=gen)
+    if args.data == "text":
+        return torch.from_numpy(synth.text_bytes(U, synth.SEED_TEXT + g)).to(dev)
+    seg = 64 << 20
+    assert U % seg == 0, "mixed units are whole 64 MiB segments"
+    return torch.from_numpy(synth.mixed_bytes(U, synth.SEED_MIXED, seg, first_segment=g * (U // seg))).to(dev)
+
+
+def bench_units(args, world: int):
+    """N ranks, one logical stream (SURVEY.md section 8(e), config C4's layout):
+    world x units-per-gpu units of U = mib/units-per-gpu MiB, unit g on rank
+    g mod world; every unit buffer = its bytes + the tail halo (the first
+    bz2mi_unit_halo bytes of unit g+1).  One step = the whole stream through
+    bz2mi.shard: front scans, chain (token in stream order), seed-sum
+    all-gather, Huffman, bit-offset scan, assembly and boundary settling; with
+    --gather rank0 also the ordered RCCL gather onto rank 0."""
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BZ2MI_SHARE_GPU=1: rehearsal of the N-rank protocol with every rank on
+    # cuda:0 (one-GPU box): gloo everywhere, no RCCL gather
+    share = os.environ.get("BZ2MI_SHARE_GPU") == "1"
+    if share:
+        local = 0
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(local)
+    if share:
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=dev)
+    ctl = dist.new_group(backend="gloo")
+    ensure_built()
+    import bz2mi
+    from bz2mi import shard
+    K = args.units_per_gpu
+    n = args.mib << 20
+    U = n // K
+    total = world * K
+    owners = shard.interleaved_owners(total, world)
+    H = bz2mi.unit_halo(args.level, args.unit)
+    ctx = bz2mi.Context(args.level, args.parallel, args.unit, device=local)
+    mine = [g for g in range(total) if owners[g] == rank]
+    bufs, halos, units = {}, {}, {}
+    for g in mine:
+        own = unit_bytes(args, g, U, dev)
+        h = unit_bytes(args, g + 1, U, dev)[:H] if g + 1 < total else own[:0]
+        bufs[g] = torch.cat([own, h])
+        halos[g] = int(h.numel())
+        del own, h
+        units[g] = shard.DeviceUnit(ctx, dev)
+    torch.cuda.synchronize()
+    out0 = None
+    if rank == 0:
+        bound = bz2mi.compress_bound(n * world, args.level, args.unit)
+        out0 = torch.empty(bound, dtype=torch.uint8, device=dev)
+
+    def step(gather: bool):
+        for g in mine:
+            units[g].begin(bufs[g], U, halos[g], g + 1 == total)
+        lay = shard.compress_units(units, owners, args.parallel, args.level, group=ctl)
+        settled = shard.settle(lay, ctl)
+        if gather:
+            shard.gather_stream_device(lay, settled, out0, args.level, dst=0)
+        return lay, settled
+
+    gather_in = args.gather == "rank0"
+    for _ in range(args.warmup):
+        step(gather_in)
+    torch.cuda.synchronize()
+    dist.barrier()
+    stage = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lay, settled = step(gather_in)
+        for g in mine:
+            for k, v in units[g].timings().items():
+                stage[k] = stage.get(k, 0.0) + v
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if share else dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    # the ordered gather onto rank 0, timed once (outside the steps unless --gather rank0)
+    gather_ms = None
+    if not share:
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter()
+        shard.gather_stream_device(lay, settled, out0, args.level, dst=0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+    verified = None
+    if rank == 0 and not args.no_verify and not share:
+        import bz2
+        head = out0[: min(lay.stream_bytes, 4 << 20)].cpu().numpy().tobytes()
+        d = bz2.BZ2Decompressor()
+        try:
+            got = d.decompress(head, max_length=2 << 20)
+            verified = bool(len(got) > 0 and got == bufs[0][: len(got)].cpu().numpy().tobytes())
+        except Exception:
+            verified = False
+    if rank == 0:
+        steps = args.steps
+        ms_step = dt / steps * 1e3
+        tot_in = n * world
+        value = tot_in * steps / dt / 1e6
+        out_bytes = lay.stream_bytes
+        achieved = (tot_in + out_bytes) / (ms_step * 1e-3) / 1e9
+        peak = HBM_PEAK_GBS * world
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"C4 layout: ONE .bz2 stream of {world} x {args.mib} MiB "
+                                   f"({WORKLOAD_DATA[args.data]}), {total} units of {U >> 20} MiB interleaved over "
+                                   f"{world} ranks (unit g on rank g mod {world}), blocks sharded by unit; output "
+                                   "bit-identical to the one-device stream",
+                       "level": args.level, "block_size": args.level * args.unit, "parallel_blocks": args.parallel,
+                       "input_bytes_per_gpu": n, "output_bytes": int(out_bytes), "ratio": round(out_bytes / tot_in, 5),
+                       "blocks": int(sum(lay.nblocks)), "parallelism": f"dp{world} (block shards of one stream)",
+                       "gather_in_step": gather_in, "decode_check": verified,
+                       "shared_gpu_rehearsal": share},
+            "roofline": {"bound": "hbm", "kernel": "pipeline (all stages, SURVEY 8(d): (N_in + N_out) / t)",
+                         "achieved": round(achieved, 2), "peak": peak, "unit": "GB/s",
+                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "stage_ms_rank0": {k: round(v / steps, 3) for k, v in stage.items()}},
+            "gather": None if gather_ms is None else {
+                "ms": round(gather_ms, 3), "bytes": int(out_bytes),
+                "what": "ordered RCCL point-to-point gather of the settled stream onto rank 0 (once, after the timed "
+                        "steps)" if not gather_in else "inside every step",
+                "value_with_gather": round(tot_in / ((ms_step + (0 if gather_in else gather_ms)) * 1e-3) / 1e6, 2)},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+WORKLOAD_DATA = {"random": "random bytes, unit g seeded 0x5EED0001+g", "text": "word-Markov text, unit g seeded "
+                 "0x5EED0002+g", "mixed": "C4 mixed-entropy segments, seed 0x5EED0003"}
 
 
 def bench_decompress(args, ctx, x, n, out, cap, world, rank, dev):

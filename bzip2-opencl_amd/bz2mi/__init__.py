@@ -32,7 +32,8 @@ EXPORTS = (
     "bz2mi_compress_bound", "bz2mi_compress_rle1", "bz2mi_finish", "bz2mi_compress_blocks",
     "bz2mi_compress", "bz2mi_compress_device", "bz2mi_last_timings", "bz2mi_blocks_done",
     "bz2mi_last_stats", "bz2mi_dcreate", "bz2mi_ddestroy", "bz2mi_decompress", "bz2mi_decompress_device",
-    "bz2mi_dlast_timings",
+    "bz2mi_dlast_timings", "bz2mi_unit_halo", "bz2mi_unit_create", "bz2mi_unit_destroy", "bz2mi_unit_begin",
+    "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode", "bz2mi_unit_assemble", "bz2mi_unit_timings",
 )
 
 _lib = None
@@ -88,6 +89,21 @@ def lib() -> ctypes.CDLL:
                                           c.POINTER(c.c_size_t), c.c_void_p]
     L.bz2mi_dlast_timings.restype = c.c_int
     L.bz2mi_dlast_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
+    L.bz2mi_unit_halo.restype = c.c_size_t
+    L.bz2mi_unit_halo.argtypes = [c.c_int, c.c_int]
+    L.bz2mi_unit_create.restype = c.c_void_p
+    L.bz2mi_unit_create.argtypes = [c.c_void_p]
+    L.bz2mi_unit_destroy.argtypes = [c.c_void_p]
+    L.bz2mi_unit_begin.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_size_t, c.c_int, c.c_void_p]
+    L.bz2mi_unit_chain.argtypes = [c.c_void_p, c.c_uint64, c.c_uint64, c.POINTER(c.c_uint64), c.POINTER(c.c_uint64)]
+    L.bz2mi_unit_sums.argtypes = [c.c_void_p, c.c_void_p]
+    L.bz2mi_unit_encode.argtypes = [c.c_void_p, c.c_void_p, c.POINTER(c.c_uint64), c.POINTER(c.c_uint32)]
+    L.bz2mi_unit_assemble.argtypes = [c.c_void_p, c.c_uint64, c.c_uint32, c.c_int, c.c_void_p, c.c_size_t,
+                                      c.POINTER(c.c_size_t)]
+    L.bz2mi_unit_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
+    for name in ("bz2mi_unit_begin", "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode",
+                 "bz2mi_unit_assemble", "bz2mi_unit_timings"):
+        getattr(L, name).restype = c.c_int
     # debugging entry points (not in include/bz2mi.h)
     L.bz2mi_debug_selftest.restype = c.c_int
     L.bz2mi_debug_selftest.argtypes = [c.POINTER(c.c_uint32), c.c_int]
@@ -189,10 +205,11 @@ class Context:
         return res
 
     def compress_device(self, d_in_ptr: int, n: int, d_out_ptr: int, cap: int, stream: int = 0) -> int:
-        """Device-resident whole stream; returns the compressed size."""
+        """Device-resident whole stream; returns the compressed size.  `stream`
+        is the hipStream_t the input was written on (0: the null stream)."""
         out_len = ctypes.c_size_t(0)
         _check(lib().bz2mi_compress_device(self._h, d_in_ptr, n, d_out_ptr, cap, ctypes.byref(out_len),
-                                           stream or None))
+                                           ctypes.c_void_p(stream)))
         return out_len.value
 
     def stats(self):
@@ -206,6 +223,69 @@ class Context:
         arr = (ctypes.c_float * 6)()
         _check(lib().bz2mi_last_timings(self._h, arr))
         return dict(zip(("front", "bwt", "mtf", "seed", "huffman", "assemble"), list(arr)))
+
+
+def unit_halo(level: int = 9, unit: int = 10000) -> int:
+    """Tail-halo bytes a stream unit needs (bz2mi_unit_halo)."""
+    return int(lib().bz2mi_unit_halo(level, unit))
+
+
+class Unit:
+    """A bz2mi_unit: one contiguous piece of a logical stream (include/bz2mi.h
+    "one logical stream compressed in units"; driven by bz2mi.shard)."""
+
+    def __init__(self, ctx: Context):
+        L = lib()
+        h = L.bz2mi_unit_create(ctx.handle)
+        if not h:
+            raise RuntimeError(L.bz2mi_last_error().decode(errors="replace"))
+        self._h = h
+        self.ctx = ctx  # keeps the context alive
+        self.parallel = ctx.parallel
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().bz2mi_unit_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def begin(self, d_ptr: int, n_own: int, n_halo: int, flags: int = 0, stream: int = 0) -> None:
+        _check(lib().bz2mi_unit_begin(self._h, d_ptr, n_own, n_halo, flags, ctypes.c_void_p(stream)))
+
+    def chain(self, entry: int, first_block: int):
+        ex = ctypes.c_uint64(0)
+        nb = ctypes.c_uint64(0)
+        _check(lib().bz2mi_unit_chain(self._h, entry, first_block, ctypes.byref(ex), ctypes.byref(nb)))
+        return ex.value, nb.value
+
+    def sums(self):
+        import numpy as np
+        out = np.zeros(self.parallel * 258, dtype=np.uint32)
+        _check(lib().bz2mi_unit_sums(self._h, out.ctypes.data))
+        return out
+
+    def encode(self, carried):
+        import numpy as np
+        c = np.ascontiguousarray(carried, dtype=np.uint32)
+        bits = ctypes.c_uint64(0)
+        crc = ctypes.c_uint32(0)
+        _check(lib().bz2mi_unit_encode(self._h, c.ctypes.data, ctypes.byref(bits), ctypes.byref(crc)))
+        return bits.value, crc.value
+
+    def assemble(self, bit_offset: int, crc_before: int, flags: int, d_out_ptr: int, cap: int) -> int:
+        n = ctypes.c_size_t(0)
+        _check(lib().bz2mi_unit_assemble(self._h, bit_offset, crc_before, flags, d_out_ptr, cap, ctypes.byref(n)))
+        return n.value
+
+    def timings(self):
+        arr = (ctypes.c_float * 6)()
+        _check(lib().bz2mi_unit_timings(self._h, arr))
+        return dict(zip(("front", "chain", "bwt", "mtf", "huffman", "assemble"), list(arr)))
 
 
 class DecompressError(RuntimeError):
@@ -273,7 +353,7 @@ class Decompressor:
         on a short buffer RuntimeError names the size needed)."""
         out_len = ctypes.c_size_t(0)
         rc = lib().bz2mi_decompress_device(self._h, d_in_ptr, n, d_out_ptr, cap, ctypes.byref(out_len),
-                                           stream or None)
+                                           ctypes.c_void_p(stream) if stream else None)
         if rc == BZ2MI_ESPACE:
             raise RuntimeError(f"output buffer too small: {out_len.value} bytes needed")
         if rc != BZ2MI_OK:

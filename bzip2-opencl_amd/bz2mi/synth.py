@@ -99,15 +99,21 @@ def small_alphabet_bytes(n: int, seed: int = SEED_MIXED, k: int = 4) -> np.ndarr
     return alpha[rng.integers(0, len(alpha), size=n)]
 
 
-def mixed_bytes(n: int, seed: int = SEED_MIXED, segment: int = 64 << 20) -> np.ndarray:
-    """C4: rotate segments of random, text, run-heavy and small-alphabet data."""
+def mixed_segment(i: int, m: int, seed: int = SEED_MIXED) -> np.ndarray:
+    """Segment i (m bytes) of the C4 stream: random, text, runs, ACGT in turn."""
     gens = [random_bytes, text_bytes, runs_bytes, small_alphabet_bytes]
+    return gens[i % 4](m, seed + i)
+
+
+def mixed_bytes(n: int, seed: int = SEED_MIXED, segment: int = 64 << 20, first_segment: int = 0) -> np.ndarray:
+    """C4: rotate segments of random, text, run-heavy and small-alphabet data
+    (the stream from segment `first_segment` on: any rank can make its part)."""
     out = np.empty(n, dtype=np.uint8)
     pos = 0
-    i = 0
+    i = first_segment
     while pos < n:
         m = min(segment, n - pos)
-        out[pos:pos + m] = gens[i % 4](m, seed + i)
+        out[pos:pos + m] = mixed_segment(i, m, seed)
         pos += m
         i += 1
     return out

@@ -12,151 +12,21 @@
 
 #include "../../include/bz2mi.h"
 #include "common.hpp"
+#include "host.hpp"
 #include "kernels.hpp"
 #include "rle1.hpp"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const std::string& msg) {
+// shared with the decoder's host code (dapi.hip) and the shard launcher (shard.hip)
+int bz2mi_set_error(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
 
-}  // namespace
-
-// shared with the decoder's host code (dapi.hip)
-int bz2mi_set_error(int code, const std::string& msg) { return fail(code, msg); }
-
-namespace {
-
-#define HIPCHECK(expr)                                                                        \
-    do {                                                                                      \
-        hipError_t e_ = (expr);                                                               \
-        if (e_ != hipSuccess)                                                                 \
-            return fail(BZ2MI_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));   \
-    } while (0)
-
-template <class T>
-int dalloc(T** p, size_t count) {
-    if (*p) {
-        (void)hipFree(*p);
-        *p = nullptr;
-    }
-    if (count == 0) count = 1;
-    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
-    if (e != hipSuccess) {
-        *p = nullptr;
-        return fail(BZ2MI_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
-    }
-    return BZ2MI_OK;
-}
-
-}  // namespace
-
-// Device buffers of one batch of blocks (RLE1 input to Huffman payloads).
-// The pipelined compress_device keeps kSets of them in flight.
-struct Batch {
-    int cap = 0;  // blocks
-    uint8_t* d_blocks = nullptr;
-    uint32_t* d_lens = nullptr;
-    uint32_t* d_crc = nullptr;
-    uint8_t* d_bwt = nullptr;
-    uint32_t* d_orig = nullptr;
-    // BWT (bwt.hip): per-block SA, group lists, counters
-    uint32_t* d_sa = nullptr;
-    uint32_t* d_bcnt = nullptr;  // [0, 64) small-queue shard counts, [64 + 64 d) level-d queue shard counts,
-                                 // [768] blocks with groups, [769] doubling pull
-                                 // counter, [8 + d] level-d queue entries
-    uint32_t* d_ngroups = nullptr;
-    uint32_t* d_p2list = nullptr;
-    bz2mi::BwtSeg* d_groups = nullptr;
-    // MTF / Huffman
-    uint16_t* d_mtf = nullptr;
-    uint32_t* d_mtflen = nullptr;
-    uint32_t* d_alpha = nullptr;
-    uint32_t* d_hist = nullptr;
-    uint32_t* d_present = nullptr;
-    uint32_t* d_seed = nullptr;
-    uint32_t* d_payload = nullptr;
-    uint64_t* d_pbits = nullptr;
-    uint64_t* d_offs = nullptr;
-    // pipeline hand-offs: stage A done, MTF done, buffers free again
-    hipEvent_t evA = nullptr, evM = nullptr, evFree = nullptr;
-
-    std::vector<void*> ptrs() const {
-        return {d_blocks, d_lens, d_crc, d_bwt, d_orig, d_sa, d_bcnt, d_ngroups, d_p2list, d_groups, d_mtf, d_mtflen, d_alpha, d_hist, d_present, d_seed, d_payload,
-                d_pbits, d_offs};
-    }
-};
-
-constexpr int kSets = 3;
-
-struct bz2mi_ctx {
-    int level = 9, p = 10, unit = 10000, S = 90000, device = 0;
-    size_t stride = 0;           // device bytes per block slot
-    size_t mtf_stride = 0;       // uint16 per block
-    size_t payload_words = 0;    // uint32 per block
-    hipStream_t stream = nullptr;  // front end and the host-driven entry points
-    hipStream_t sA = nullptr, sM = nullptr, sB = nullptr;  // pipeline: RLE1+CRC+BWT / MTF / Huffman+assembly
-    bool own_stream = false;
-    int cus = 256;
-    int bwt_slots = 0;
-    int batch_blocks = 0;  // blocks per pipelined batch (0: from the block size)
-    bool want_stats = false;
-
-    Batch sets[kSets];
-    uint32_t* d_out = nullptr;   // staging for the host-driven assembly
-    size_t out_words = 0;
-    uint8_t* d_scratch = nullptr;  // BWT workgroup slots (one BWT runs at a time: stream sA)
-    uint64_t* d_sq = nullptr;      // BWT small-segment queue (all blocks of a batch)
-    bz2mi::BwtItem* d_lq[2] = {nullptr, nullptr};  // BWT level queues (ping-pong)
-    uint64_t* d_tq[2] = {nullptr, nullptr};         // BWT per-block tie-group lists (ping-pong)
-    uint32_t* d_tc = nullptr;                       // their per-block counts (2 x blocks)
-    int small_grid = 0;                             // resident workgroups of bwt_small_kernel
-    int level_slots = 0;                            // resident workgroups of bwt_level_kernel
-    uint8_t* d_lscratch = nullptr;                  // their scratch slots
-    int wlevel_grid = 0;                            // resident workgroups of bwt_wlevel_kernel
-    uint32_t* d_lspill = nullptr;                   // wave-level stage spill (one word per rotation of a batch)
-    uint32_t* d_scb = nullptr;                      // per-block small-batch counts (LDS-text path)
-    int bwtq_blocks = 0;           // capacity of the queues in blocks
-    uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
-    uint32_t* d_crctab = nullptr;
-    bz2mi::StreamDev* d_sd = nullptr;
-    unsigned long long* d_vol = nullptr;  // [3] volumes of the last compress_device call
-    bz2mi::StreamDev h_sd{};
-    uint8_t* d_ostage = nullptr;   // aligned output staging for unaligned destinations
-    size_t ostage_cap = 0;
-    // front-end buffers (device RLE1 path)
-    size_t fe_n = 0;
-    uint8_t* d_in = nullptr;        // staging for host input
-    size_t in_cap = 0;
-    uint8_t* d_cost = nullptr;
-    uint8_t* d_dmap = nullptr;
-    uint4* d_summ = nullptr;
-    uint64_t* d_rsb = nullptr;
-    uint32_t* d_ccost = nullptr;
-    uint64_t* d_fc = nullptr;
-    uint64_t* d_bnd = nullptr;
-    uint64_t* d_starts = nullptr;
-    uint64_t* d_nb = nullptr;
-    size_t fe_maxb = 0;
-    hipEvent_t ev[8] = {};
-    std::vector<hipEvent_t> tev;  // per-batch stage timing events (12 per batch)
-    float last_ms[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-
-    // stream state of the host-driven path (OutputStream.hpp:39-44)
-    uint64_t blocks_done = 0;
-    uint32_t stream_crc = 0;
-    uint64_t carry = 0;      // MSB-aligned pending bits
-    int carry_bits = 0;
-    bool header_done = false;
-    bool finished = false;
-
-    std::vector<uint8_t> h_stage;
-};
+using namespace bz2mi::host;
 
 namespace {
 
@@ -177,6 +47,19 @@ bool sync_debug() {
             fprintf(stderr, "[bz2mi] %s done: %s\n", name, hipGetErrorString(e2_));   \
         }                                                                             \
     } while (0)
+
+}  // namespace
+
+namespace bz2mi {
+namespace host {
+
+void free_batch(Batch& t) {
+    for (void* p : t.ptrs())
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : {t.evA, t.evM, t.evFree})
+        if (e) (void)hipEventDestroy(e);
+    t = Batch{};
+}
 
 int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks) {
     if (nblocks <= t.cap) return BZ2MI_OK;
@@ -211,25 +94,14 @@ int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks) {
     return BZ2MI_OK;
 }
 
-// host-driven paths: batch set 0 plus the assembly staging buffer
-int ensure_capacity(bz2mi_ctx* c, int nblocks) {
-    int r;
-    if ((r = ensure_batch(c, c->sets[0], nblocks))) return r;
-    const size_t words = (size_t)c->sets[0].cap * (c->payload_words + 4) + 64;
-    if (words > c->out_words) {
-        if ((r = dalloc(&c->d_out, words))) return r;
-        c->out_words = words;
-    }
-    return BZ2MI_OK;
-}
-
 // ---- the stages of one batch, each on its stream
 // RLE1 emission + block CRCs of blocks [first, first+cnt) of the front end
-int stage_front(bz2mi_ctx* c, Batch& t, const uint8_t* d_x, size_t n, uint64_t first, uint64_t cnt, hipStream_t s) {
+int stage_front(bz2mi_ctx* c, Batch& t, const FrontBufs& f, const uint8_t* d_x, size_t n, uint64_t first,
+                uint64_t cnt, hipStream_t s) {
     using namespace bz2mi;
-    hipLaunchKernelGGL(fe_rle1_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts, first,
+    hipLaunchKernelGGL(fe_rle1_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, f.d_starts, first,
                        cnt, t.d_blocks, c->stride, t.d_lens);
-    hipLaunchKernelGGL(fe_crc_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, c->d_starts, first, cnt,
+    hipLaunchKernelGGL(fe_crc_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, f.d_starts, first, cnt,
                        t.d_crc, c->d_crctab);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("front-rle1");
@@ -350,10 +222,10 @@ int stage_mtf(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     return BZ2MI_OK;
 }
 
-int stage_seed(bz2mi_ctx* c, Batch& t, int nb, uint64_t first_block, hipStream_t s) {
+int stage_seed(bz2mi_ctx* c, Batch& t, int nb, uint64_t first_block, uint32_t* state, hipStream_t s) {
     using namespace bz2mi;
     const int ne = c->p * kMaxAlpha;
-    hipLaunchKernelGGL(seed_kernel, dim3((ne + 255) / 256), dim3(256), 0, s, t.d_hist, t.d_seed, c->d_state, nb, c->p,
+    hipLaunchKernelGGL(seed_kernel, dim3((ne + 255) / 256), dim3(256), 0, s, t.d_hist, t.d_seed, state, nb, c->p,
                        first_block);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("seed");
@@ -370,6 +242,93 @@ int stage_huffman(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     return BZ2MI_OK;
 }
 
+int ensure_front(FrontBufs& f, int S, size_t n) {
+    if (n <= f.n_cap && f.d_cost) return BZ2MI_OK;
+    const size_t cap = std::max(n, (size_t)1 << 20);
+    const size_t nc = (cap + bz2mi::kFeChunk - 1) / bz2mi::kFeChunk;
+    const size_t maxb = (cap + cap / 4) / (size_t)(S - 5) + 8;
+    int r;
+    if ((r = dalloc(&f.d_cost, cap + 64))) return r;
+    if ((r = dalloc(&f.d_dmap, cap + cap / 4 + 4096))) return r;
+    if ((r = dalloc(&f.d_summ, nc + 1))) return r;
+    if ((r = dalloc(&f.d_rsb, nc + 2))) return r;
+    if ((r = dalloc(&f.d_ccost, nc + 1))) return r;
+    if ((r = dalloc(&f.d_fc, nc + 2))) return r;
+    if ((r = dalloc(&f.d_bnd, maxb + 2))) return r;
+    if ((r = dalloc(&f.d_starts, maxb + 3))) return r;
+    if ((r = dalloc(&f.d_nb, 4))) return r;
+    f.n_cap = cap;
+    f.maxb = maxb;
+    return BZ2MI_OK;
+}
+
+void free_front(FrontBufs& f) {
+    for (void* p : f.ptrs())
+        if (p) (void)hipFree(p);
+    f = FrontBufs{};
+}
+
+int enqueue_front_scan(FrontBufs& f, const uint8_t* d_x, size_t n, hipStream_t s) {
+    using namespace bz2mi;
+    if (n == 0) return BZ2MI_OK;
+    const uint64_t nc = (n + kFeChunk - 1) / kFeChunk;
+    const dim3 g4((unsigned)((nc + 3) / 4));
+    hipLaunchKernelGGL(fe_summary_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, f.d_summ);
+    hipLaunchKernelGGL(fe_runscan_kernel, dim3(1), dim3(kFeScanThreads), 0, s, f.d_summ, nc, f.d_rsb);
+    hipLaunchKernelGGL(fe_cost_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, f.d_summ, f.d_rsb, f.d_cost,
+                       f.d_ccost);
+    hipLaunchKernelGGL(fe_costscan_kernel, dim3(1), dim3(kFeScanThreads), 0, s, f.d_ccost, nc, f.d_fc);
+    hipLaunchKernelGGL(fe_dmap_kernel, g4, dim3(256), 0, s, d_x, f.d_cost, (uint64_t)n, nc, f.d_fc, f.d_dmap);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("front-scan");
+    return BZ2MI_OK;
+}
+
+int run_chain(bz2mi_ctx* c, FrontBufs& f, const uint8_t* d_x, size_t n, size_t n_own, uint64_t entry, bool ends,
+              uint64_t* nb_out, uint64_t* exit_out, hipStream_t s) {
+    using namespace bz2mi;
+    const uint64_t nc = (n + kFeChunk - 1) / kFeChunk;
+    hipLaunchKernelGGL(fe_chain_kernel, dim3(1), dim3(kFeChainThreads), 0, s, d_x, f.d_cost, f.d_fc, f.d_summ, f.d_dmap,
+                       (uint64_t)n, nc, c->S, (uint64_t)n_own, entry, ends ? 1 : 0, f.d_bnd, (uint64_t)f.maxb,
+                       f.d_nb);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("front-chain");
+    uint64_t hv[2] = {0, 0};
+    HIPCHECK(hipMemcpyAsync(hv, f.d_nb, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    if (hv[1] == 1) return fail(BZ2MI_EINVAL, "stream unit: the last block runs past the tail halo");
+    if (hv[0] == 0 || hv[0] > f.maxb || hv[1] != 0)
+        return fail(BZ2MI_EDEVICE, "front end produced an invalid block count");
+    const uint64_t nb = hv[0];
+    hipLaunchKernelGGL(fe_resolve_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, d_x, f.d_cost, f.d_fc,
+                       f.d_summ, (uint64_t)n, nc, (uint64_t)n_own, entry, f.d_bnd, f.d_nb, f.d_starts);
+    HIPCHECK(hipGetLastError());
+    STAGE_DONE("front-resolve");
+    *nb_out = nb;
+    if (exit_out) {
+        HIPCHECK(hipMemcpyAsync(exit_out, f.d_nb + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+    }
+    return BZ2MI_OK;
+}
+
+}  // namespace host
+}  // namespace bz2mi
+
+namespace {
+
+// host-driven paths: batch set 0 plus the assembly staging buffer
+int ensure_capacity(bz2mi_ctx* c, int nblocks) {
+    int r;
+    if ((r = ensure_batch(c, c->sets[0], nblocks))) return r;
+    const size_t words = (size_t)c->sets[0].cap * (c->payload_words + 4) + 64;
+    if (words > c->out_words) {
+        if ((r = dalloc(&c->d_out, words))) return r;
+        c->out_words = words;
+    }
+    return BZ2MI_OK;
+}
+
 // Host-driven kernel sequence for `nb` RLE1 blocks already in set 0
 // (d_blocks/d_lens/d_crc), all on the context stream.  Produces
 // d_payload/d_pbits.
@@ -383,7 +342,7 @@ int run_blocks(bz2mi_ctx* c, int nb) {
     HIPCHECK(hipEventRecord(c->ev[1], s));
     if ((r = stage_mtf(c, t, nb, s))) return r;
     HIPCHECK(hipEventRecord(c->ev[2], s));
-    if ((r = stage_seed(c, t, nb, c->blocks_done, s))) return r;
+    if ((r = stage_seed(c, t, nb, c->blocks_done, c->d_state, s))) return r;
     HIPCHECK(hipEventRecord(c->ev[3], s));
     if ((r = stage_huffman(c, t, nb, s))) return r;
     HIPCHECK(hipEventRecord(c->ev[4], s));
@@ -451,26 +410,6 @@ int assemble(bz2mi_ctx* c, int nb, bool final_, uint8_t* out, size_t cap, size_t
     return BZ2MI_OK;
 }
 
-int ensure_frontend(bz2mi_ctx* c, size_t n) {
-    if (n <= c->fe_n && c->d_cost) return BZ2MI_OK;
-    const size_t cap = std::max(n, (size_t)1 << 20);
-    const size_t nc = (cap + bz2mi::kFeChunk - 1) / bz2mi::kFeChunk;
-    const size_t maxb = (cap + cap / 4) / (size_t)(c->S - 5) + 8;
-    int r;
-    if ((r = dalloc(&c->d_cost, cap + 64))) return r;
-    if ((r = dalloc(&c->d_dmap, cap + cap / 4 + 4096))) return r;
-    if ((r = dalloc(&c->d_summ, nc + 1))) return r;
-    if ((r = dalloc(&c->d_rsb, nc + 2))) return r;
-    if ((r = dalloc(&c->d_ccost, nc + 1))) return r;
-    if ((r = dalloc(&c->d_fc, nc + 2))) return r;
-    if ((r = dalloc(&c->d_bnd, maxb + 2))) return r;
-    if ((r = dalloc(&c->d_starts, maxb + 3))) return r;
-    if ((r = dalloc(&c->d_nb, 2))) return r;
-    c->fe_n = cap;
-    c->fe_maxb = maxb;
-    return BZ2MI_OK;
-}
-
 void reset_stream(bz2mi_ctx* c) {
     c->blocks_done = 0;
     c->stream_crc = 0;
@@ -506,30 +445,13 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
     hipStream_t s = c->stream;
     int r;
     reset_stream(c);
-    if ((r = ensure_frontend(c, n))) return r;
-    const uint64_t nc = (n + kFeChunk - 1) / kFeChunk;
+    if ((r = ensure_front(c->fe, c->S, n))) return r;
     uint64_t nb = 0;
     (void)hipGetLastError();
     HIPCHECK(hipEventRecord(c->ev[6], s));
     if (n > 0) {
-        const dim3 g4((unsigned)((nc + 3) / 4));
-        hipLaunchKernelGGL(fe_summary_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, c->d_summ);
-        hipLaunchKernelGGL(fe_runscan_kernel, dim3(1), dim3(kFeScanThreads), 0, s, c->d_summ, nc, c->d_rsb);
-        hipLaunchKernelGGL(fe_cost_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, c->d_summ, c->d_rsb, c->d_cost,
-                           c->d_ccost);
-        hipLaunchKernelGGL(fe_costscan_kernel, dim3(1), dim3(kFeScanThreads), 0, s, c->d_ccost, nc, c->d_fc);
-        hipLaunchKernelGGL(fe_dmap_kernel, g4, dim3(256), 0, s, d_x, c->d_cost, (uint64_t)n, nc, c->d_fc, c->d_dmap);
-        hipLaunchKernelGGL(fe_chain_kernel, dim3(1), dim3(kFeChainThreads), 0, s, d_x, c->d_cost, c->d_fc, c->d_summ, c->d_dmap,
-                           (uint64_t)n, nc, c->S, c->d_bnd, (uint64_t)c->fe_maxb, c->d_nb);
-        HIPCHECK(hipGetLastError());
-        STAGE_DONE("front-chain");
-        HIPCHECK(hipMemcpyAsync(&nb, c->d_nb, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        HIPCHECK(hipStreamSynchronize(s));
-        if (nb == 0 || nb > c->fe_maxb) return fail(BZ2MI_EDEVICE, "front end produced an invalid block count");
-        hipLaunchKernelGGL(fe_resolve_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, d_x, c->d_cost, c->d_fc,
-                           c->d_summ, (uint64_t)n, nc, c->d_bnd, c->d_nb, c->d_starts);
-        HIPCHECK(hipGetLastError());
-        STAGE_DONE("front-resolve");
+        if ((r = enqueue_front_scan(c->fe, d_x, n, s))) return r;
+        if ((r = run_chain(c, c->fe, d_x, n, n, 0, true, &nb, nullptr, s))) return r;
     }
     HIPCHECK(hipEventRecord(c->ev[7], s));
     // batches
@@ -568,7 +490,7 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
         if (cnt) {
             if (k >= (uint64_t)kSets) HIPCHECK(hipStreamWaitEvent(c->sA, t.evFree, 0));
             HIPCHECK(hipEventRecord(te[0], c->sA));
-            if ((r = stage_front(c, t, d_x, n, first, cnt, c->sA))) return r;
+            if ((r = stage_front(c, t, c->fe, d_x, n, first, cnt, c->sA))) return r;
             HIPCHECK(hipEventRecord(te[1], c->sA));
             HIPCHECK(hipEventRecord(te[2], c->sA));
             if ((r = stage_bwt(c, t, (int)cnt, c->sA))) return r;
@@ -581,7 +503,7 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
             HIPCHECK(hipEventRecord(t.evM, c->sM));
             HIPCHECK(hipStreamWaitEvent(c->sB, t.evM, 0));
             HIPCHECK(hipEventRecord(te[6], c->sB));
-            if ((r = stage_seed(c, t, (int)cnt, first, c->sB))) return r;
+            if ((r = stage_seed(c, t, (int)cnt, first, c->d_state, c->sB))) return r;
             HIPCHECK(hipEventRecord(te[7], c->sB));
             HIPCHECK(hipEventRecord(te[8], c->sB));
             if ((r = stage_huffman(c, t, (int)cnt, c->sB))) return r;
@@ -695,7 +617,8 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->sA, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->sM, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->sB, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->sB, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->sF, hipStreamNonBlocking) != hipSuccess) {
         fail(BZ2MI_EDEVICE, "hipStreamCreate failed");
         bz2mi_destroy(c);
         return nullptr;
@@ -744,31 +667,32 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     c->batch_blocks = std::min(16384, std::max(64, (int)((1536u << 20) / (unsigned)c->S)));
     if (const char* e = getenv("BZ2MI_BATCH_BLOCKS")) c->batch_blocks = std::max(1, atoi(e));
     for (auto& e : c->ev) (void)hipEventCreate(&e);
+    if (hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess) {
+        fail(BZ2MI_EDEVICE, "hipEventCreate failed");
+        bz2mi_destroy(c);
+        return nullptr;
+    }
     return c;
 }
 
 void bz2mi_destroy(bz2mi_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB})
+    for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB, c->sF})
         if (st) (void)hipStreamSynchronize(st);
     std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_sq, c->d_lq[0], c->d_lq[1], c->d_tq[0], c->d_tq[1],
-                               c->d_tc, c->d_lscratch, c->d_lspill, c->d_scb, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
-                               c->d_cost, c->d_dmap, c->d_summ, c->d_rsb, c->d_ccost, c->d_fc, c->d_bnd,
-                               c->d_starts, c->d_nb};
-    for (const Batch& t : c->sets) {
-        for (void* p : t.ptrs()) ptrs.push_back(p);
-        for (hipEvent_t e : {t.evA, t.evM, t.evFree})
-            if (e) (void)hipEventDestroy(e);
-    }
+                               c->d_tc, c->d_lscratch, c->d_lspill, c->d_scb, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in};
+    for (Batch& t : c->sets) free_batch(t);
+    free_front(c->fe);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->own_stream)
-        for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB})
+        for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB, c->sF})
             if (st) (void)hipStreamDestroy(st);
     delete c;
 }
@@ -879,8 +803,10 @@ int bz2mi_compress_device(bz2mi_ctx* c, const void* d_in, size_t n, void* d_out,
                           void* hip_stream) {
     if (!c || !out_len || (n && !d_in) || !d_out) return fail(BZ2MI_EINVAL, "null argument");
     HIPCHECK(hipSetDevice(c->device));
-    hipStream_t user = (hipStream_t)hip_stream;
-    if (user) HIPCHECK(hipStreamSynchronize(user));  // inputs written on the caller's stream are complete
+    // inputs written on the caller's stream (NULL: the null stream, where torch
+    // writes by default) are complete before the context's streams read them
+    HIPCHECK(hipEventRecord(c->ev_in, (hipStream_t)hip_stream));
+    HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_in, 0));
     int r = compress_device_impl(c, (const uint8_t*)d_in, n, (uint8_t*)d_out, cap, out_len);
     if (r) return r;
     return BZ2MI_OK;

@@ -93,6 +93,7 @@ struct bz2mi_dctx {
     uint8_t* d_out = nullptr;  // staging for host output
     size_t out_cap = 0;
     hipEvent_t ev[6] = {};
+    hipEvent_t ev_in = nullptr;  // null stream -> decoder stream hand-off
     float ms[6] = {0, 0, 0, 0, 0, 0};
 };
 
@@ -129,9 +130,21 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
     }
     uint32_t ncand = 0;
     DCHECK(hipMemcpyAsync(&ncand, d->d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    DCHECK(hipEventRecord(d->ev[1], s));
     DCHECK(hipStreamSynchronize(s));
-    if (ncand > d->cand_cap) return bz2mi_set_error(BZ2MI_EFORMAT, "BZip2 stream format error");
+    if (ncand > d->cand_cap) {
+        // more magic matches than the estimate (crafted input): the scan
+        // counted them all, so rescan into a buffer of the exact size
+        if ((r = grow(&d->d_cand, &d->cand_cap, ncand))) return r;
+        DCHECK(hipMemsetAsync(d->d_cnt, 0, 4 * sizeof(uint32_t), s));
+        const uint64_t words = (n + 7) / 8;
+        hipLaunchKernelGGL(dec_scan_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, d_in, (uint64_t)n,
+                           d->d_cand, d->d_cnt, (uint32_t)d->cand_cap);
+        DCHECK(hipGetLastError());
+        DCHECK(hipMemcpyAsync(&ncand, d->d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        DCHECK(hipStreamSynchronize(s));
+        if (ncand > d->cand_cap) return bz2mi_set_error(BZ2MI_EFORMAT, "BZip2 stream format error");
+    }
+    DCHECK(hipEventRecord(d->ev[1], s));
     std::vector<DecCand> cand(ncand);
     if (ncand) DCHECK(hipMemcpy(cand.data(), d->d_cand, ncand * sizeof(DecCand), hipMemcpyDeviceToHost));
     std::sort(cand.begin(), cand.end(), [](const DecCand& a, const DecCand& b) { return a.bitpos < b.bitpos; });
@@ -387,6 +400,7 @@ bz2mi_dctx* bz2mi_dcreate(int unit, int device) {
               hipMemcpy(d->d_crctab, bz2mi::kCrc.t.data(), 256 * sizeof(uint32_t), hipMemcpyHostToDevice) ==
                   hipSuccess;
     for (auto& e : d->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&d->ev_in, hipEventDisableTiming) == hipSuccess;
     // x^(8 * 2^k) mod P for the CRC combination
     uint32_t xp[64];
     {
@@ -417,10 +431,11 @@ void bz2mi_ddestroy(bz2mi_dctx* d) {
     for (void* p : {(void*)d->d_crctab, (void*)d->d_cnt, (void*)d->d_cand, (void*)d->d_ids, (void*)d->d_bwt,
                     (void*)d->d_syms, (void*)d->d_symmap, (void*)d->d_tabs, (void*)d->d_info, (void*)d->d_blocks, (void*)d->d_merged,
                     (void*)d->d_marks, (void*)d->d_rle1, (void*)d->d_cstate, (void*)d->d_olen, (void*)d->d_ooff,
-                    (void*)d->d_crc, (void*)d->d_in, (void*)d->d_out})
+                    (void*)d->d_crc, (void*)d->d_in, (void*)d->d_out, (void*)d->d_bad})
         if (p) (void)hipFree(p);
     for (auto& e : d->ev)
         if (e) (void)hipEventDestroy(e);
+    if (d->ev_in) (void)hipEventDestroy(d->ev_in);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
 }
@@ -430,6 +445,10 @@ int bz2mi_decompress_device(bz2mi_dctx* d, const void* d_in, size_t n, void* d_o
     if (!d || !out_len || (n && !d_in) || (cap && !d_out)) return bz2mi_set_error(BZ2MI_EINVAL, "null argument");
     DCHECK(hipSetDevice(d->device));
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : d->stream;
+    if (!hip_stream) {  // input written on the null stream (torch's default) is complete first
+        DCHECK(hipEventRecord(d->ev_in, nullptr));
+        DCHECK(hipStreamWaitEvent(s, d->ev_in, 0));
+    }
     const uint8_t* in = (const uint8_t*)d_in;
     if (((uintptr_t)in & 3u) != 0) {  // the bit reader loads aligned words
         int r;

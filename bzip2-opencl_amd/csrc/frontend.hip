@@ -483,21 +483,38 @@ __device__ uint64_t run_end(const FeView& f, uint64_t p) {
 
 }  // namespace
 
-// ---- K6: the block chain (one workgroup).  bnd[k] is the start of block k+1,
-// either as a target y (bit 63 clear: start = Ginv(y)) or as an explicit
-// position (bit 63 set).  *nb_out = number of blocks.
+// ---- K6: the block chain (one workgroup) of one unit of the stream: the
+// buffer holds the unit's own bytes [0, n_own) and a tail halo [n_own, n) of
+// the bytes that follow it (n_own == n: the unit ends the stream).  The
+// unit's first block starts at entry (bit 63: mid-run, i.e. x[p] == x[p-1] in
+// the whole stream); blocks follow until the next start is >= n_own.
+// bnd[j] is the end (= start of the next block) of block j, either as a target
+// y (bit 63 clear: position Ginv(y)) or as an explicit position (bit 63 set);
+// bnd[nb-1] is the unit's exit (n when the stream ends).  out[0] = nb,
+// out[1] = status (0 ok, 1 the last block runs past a halo that does not
+// reach the stream end, 2 overflow).
+// The chain depends only on the bytes from the entry on (RLE1 state restarts
+// at every block start), so a unit's front end treats its buffer as a stream
+// of its own and the entry comes from the previous unit (bz2mi_shard_chain).
 __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
                                                       const uint64_t* __restrict__ fc, const uint4* __restrict__ summ,
                                                       const uint8_t* __restrict__ dmap, uint64_t n, uint64_t nc, int S,
+                                                      uint64_t n_own, uint64_t entry, int ends,
                                                       uint64_t* __restrict__ bnd, uint64_t max_bnd,
                                                       uint64_t* __restrict__ nb_out) {
     FeView f{x, cost, fc, summ, n, nc, uniform64(fc[nc])};
-    if (n == 0) {
-        if (threadIdx.x == 0) *nb_out = 0;
+    constexpr uint64_t kExpl = 1ull << 63;
+    if (n == 0 || n_own == 0) {
+        if (threadIdx.x == 0) {
+            nb_out[0] = 0;
+            nb_out[1] = 0;
+        }
         return;
     }
-    // Ytot: targets y >= Fg(n-1) have no boundary inside the input
+    // ytot = Fg(n-1): targets y >= ytot have no start inside the buffer;
+    // ystop = Fg(n_own-1): targets y >= ystop start at or after n_own
     const uint64_t ytot = fc[nc] - cost[n - 1];
+    const uint64_t ystop = n_own >= n ? ytot : uniform64(fg_at(f, n_own - 1));
     const uint64_t lim = (uint64_t)(S - 6);
     const uint32_t jstar = (uint32_t)((S - 6) / 5 + 1);
     // Case-A steps advance y by D + S-6 (D < 16).  A round covers the next
@@ -517,11 +534,14 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
     __shared__ uint16_t jmp[kGroups * kWin];
     __shared__ uint16_t walk[kStepsR];  // offset of step m, or kDirect (bnd written by the slow path)
     __shared__ uint32_t jumped[kGroups];
-    __shared__ uint64_t ctl[4];  // next round's y (or ~0: the chain ended), k after the round, steps
+    __shared__ uint64_t ctl[6];  // next round's y, k after the round, steps, mean D, done, exit
     const int tid = threadIdx.x;
     // chain state (wave 0; uniform)
     uint64_t k = 0;
-    uint64_t y = lim;  // block 0 starts at 0 (a run start), Fg(1) = 0
+    uint64_t y = 0;
+    uint64_t status = 0;
+    bool done = false;
+    uint64_t exit_b = n | kExpl;
     uint64_t dsum = 0, dcnt = 0;  // (wave 0)
     uint64_t dfp = 8ull << 16;    // mean D, 16.16, for the window predictions
     [[maybe_unused]] int nwin = 0, nslow = 0;
@@ -531,9 +551,104 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
 #define FE_NOW() 0ull
 #endif
     unsigned long long t_tab = 0, t_ch = 0, t_bnd = 0, t_slow = 0, n_out = 0, n_mid = 0;
-    constexpr uint64_t kEnded = ~0ull;
+    // The slow path (wave 0): blocks that start inside a run (p, mid-run),
+    // block by block, until the chain is back on a run start (returns true, y
+    // set) or the unit's chain ends (returns false, exit_b set).  `direct`
+    // records a block start found here.
+    auto slow_from = [&](uint64_t p, auto&& direct) -> bool {
+        for (;;) {
+            if (k + 1 >= max_bnd) {
+                status = 2;
+                exit_b = n | kExpl;
+                return false;
+            }
+            nslow++;
+            // block starting at p, mid-run: its first run is [p, e)
+            const uint64_t e = run_end(f, p);
+            const uint64_t Lr = e - p;
+            if ((uint64_t)jstar * 255u <= Lr) {
+                const uint64_t E = p + (uint64_t)jstar * 255u;
+                if (E >= n_own) {
+                    exit_b = (E >= n ? n : E) | kExpl;
+                    if (E >= n && !ends) status = 1;
+                    return false;
+                }
+                direct(E | kExpl);
+                if (E < e) {
+                    p = E;  // still inside the run
+                    continue;
+                }
+                // E == e: a run start
+                y = fg_at(f, E + 1) + lim;
+                return true;
+            }
+            if (e >= n) {  // the run reaches the end of the buffer: last block
+                exit_b = n | kExpl;
+                if (!ends) status = 1;
+                return false;
+            }
+            const uint64_t tot = 5ull * (Lr / 255) + piece_cost((uint32_t)(Lr % 255));
+            if (tot > lim) {
+                const uint64_t E = e + 1;
+                if (E >= n_own) {
+                    exit_b = (E >= n ? n : E) | kExpl;
+                    if (E >= n && !ends) status = 1;
+                    return false;
+                }
+                direct(E | kExpl);
+                if (f.x[E] != f.x[E - 1]) {
+                    y = fg_at(f, E + 1) + lim;
+                    return true;
+                }
+                p = E;
+                continue;
+            }
+            // continue in unsplit coordinates after the run
+            y = fg_at(f, e + 1) - tot + lim;
+            return true;
+        }
+    };
+    // entry: a run start (the target of the next block follows from Fg), or
+    // mid-run (the slow path, wave 0, before the rounds)
+    {
+        const uint64_t p0 = entry & ~kExpl;
+        if (!(entry >> 63)) {
+            y = uniform64(fg_at(f, p0 + 1)) + lim;
+        } else {
+            if (tid < 64) {
+                const bool have = slow_from(p0, [&](uint64_t v) {
+                    if (tid == 0) bnd[k] = v;
+                    k++;
+                });
+                if (tid == 0) {
+                    ctl[0] = y;
+                    ctl[1] = k;
+                    ctl[4] = have ? 0 : 1;
+                    ctl[5] = exit_b;
+                    ctl[2] = status;
+                }
+            }
+            __syncthreads();
+            y = ctl[0];
+            k = ctl[1];
+            done = ctl[4] != 0;
+            exit_b = ctl[5];
+            status = ctl[2];
+            __syncthreads();
+        }
+    }
     for (;;) {
-        if (k + 1 >= max_bnd || y >= ytot) break;  // (y == kEnded too)
+        if (done) break;
+        if (k + 1 >= max_bnd) {
+            status = 2;
+            exit_b = n | kExpl;
+            break;
+        }
+        if (y >= ystop) {  // the next start is outside the unit: the exit
+            exit_b = y >= ytot ? (n | kExpl) : y;
+            if (y >= ytot && !ends) status = 1;
+            break;
+        }
         const unsigned long long tr = FE_NOW();
         BZ2MI_PHASE(g_fe_phase, nwin < 6 ? nwin : 5, nwin < 6);
         nwin++;
@@ -560,7 +675,7 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
                 const uint64_t yy = y0 + (uint64_t)q;
                 const uint32_t d = (w[q >> 2] >> (8 * (q & 3))) & 0xffu;
                 uint32_t t;
-                if (yy >= ytot) {
+                if (yy >= ystop) {
                     t = kEnd;
                 } else if (!(d & 16u)) {
                     t = kMidRun;
@@ -630,7 +745,7 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
                     }
                 }
                 if (k + 1 >= max_bnd) {
-                    y = kEnded;
+                    y = wstart_of((uint64_t)m) + o;  // (the top of the next round reports the overflow)
                     break;
                 }
                 const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)trans[m * kWin + (int)o]);
@@ -643,10 +758,7 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
                 }
                 // a terminal at step m
                 y = uniform64(wstart_of((uint64_t)m) + o);
-                if (t == kEnd) {
-                    y = kEnded;  // y >= ytot: no boundary inside the input
-                    break;
-                }
+                if (t == kEnd) break;  // y >= ystop: the exit (reported at the top of the next round)
                 if (tid == 0) walk[m] = (uint16_t)o;  // the block at y itself
                 m++;
                 k++;
@@ -668,52 +780,15 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
                     dcnt += (uint64_t)(m - 1);
                 }
                 clean = false;
-                uint64_t p = ginv(f, y);
-                bool have_y = false;
-                while (!have_y) {
-                    if (k + 1 >= max_bnd) break;
-                    nslow++;
-                    // block starting at p, mid-run: its first run is [p, e)
-                    const uint64_t e = run_end(f, p);
-                    const uint64_t Lr = e - p;
-                    if ((uint64_t)jstar * 255u <= Lr) {
-                        const uint64_t E = p + (uint64_t)jstar * 255u;
-                        if (E >= n) break;
-                        direct(E | (1ull << 63));
-                        if (E < e) {
-                            p = E;  // still inside the run
-                            continue;
-                        }
-                        // E == e: a run start
-                        y = fg_at(f, E + 1) + lim;
-                        have_y = true;
-                        continue;
-                    }
-                    if (e >= n) break;  // the run reaches the end: last block
-                    const uint64_t tot = 5ull * (Lr / 255) + piece_cost((uint32_t)(Lr % 255));
-                    if (tot > lim) {
-                        const uint64_t E = e + 1;
-                        if (E >= n) break;
-                        direct(E | (1ull << 63));
-                        if (f.x[E] != f.x[E - 1]) {
-                            y = fg_at(f, E + 1) + lim;
-                            have_y = true;
-                        } else {
-                            p = E;
-                        }
-                        continue;
-                    }
-                    // continue in unsplit coordinates after the run
-                    y = fg_at(f, e + 1) - tot + lim;
-                    have_y = true;
-                }
+                const uint64_t p = ginv(f, y);
+                const bool have_y = slow_from(p, direct);
                 t_slow += FE_NOW() - ts;
                 if (!have_y) {
-                    y = kEnded;
+                    done = true;
                     break;
                 }
                 // back in the windows?  then the chase goes on
-                if (m < kStepsR && y < ytot) {
+                if (m < kStepsR && y < ystop) {
                     const uint64_t ws = wstart_of((uint64_t)m);
                     if (y >= ws && y < ws + kWin) {
                         o = (uint32_t)(y - ws);
@@ -727,6 +802,8 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
                 ctl[1] = k;
                 ctl[2] = (uint64_t)m;
                 ctl[3] = dcnt ? (uint64_t)((float)dsum / (float)dcnt * 65536.0f) : dfp;
+                ctl[4] = done ? 1 : 0;
+                ctl[5] = exit_b | (status << 61);
             }
         }
         __syncthreads();
@@ -736,6 +813,11 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
         k = ctl[1];
         const int msteps = min((int)ctl[2], kStepsR);
         const uint64_t dfp_next = ctl[3];
+        done = ctl[4] != 0;
+        if (done) {
+            exit_b = ctl[5] & ~(3ull << 61);
+            status = (ctl[5] >> 61) & 3u;
+        }
         // replay the jumped-over steps (one thread per group)
         if (tid < kGroups && jumped[tid]) {
             uint32_t o = walk[tid * kJ];
@@ -771,27 +853,37 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
     (void)nslow;
     (void)t_tab, (void)t_ch, (void)t_bnd, (void)t_slow, (void)n_out, (void)n_mid;
 #endif
-    if (threadIdx.x == 0) *nb_out = k + 1;
+    if (threadIdx.x == 0) {
+        bnd[k] = exit_b;
+        nb_out[0] = k + 1;
+        nb_out[1] = status;
+    }
 }
 
-// ---- K7: boundary targets -> positions; starts[0] = 0, starts[nb] = n
+// ---- K7: block ends -> positions: starts[0] = entry, starts[j+1] = the end
+// of block j (bnd[j]); nb_io[2] = the exit token of the next unit
+// (starts[nb] - n_own, bit 63: mid-run), when the unit does not end the stream
 __global__ __launch_bounds__(256) void fe_resolve_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
                                                          const uint64_t* __restrict__ fc, const uint4* __restrict__ summ,
-                                                         uint64_t n, uint64_t nc, const uint64_t* __restrict__ bnd,
-                                                         const uint64_t* __restrict__ nb_in, uint64_t* __restrict__ starts) {
+                                                         uint64_t n, uint64_t nc, uint64_t n_own, uint64_t entry,
+                                                         const uint64_t* __restrict__ bnd, uint64_t* __restrict__ nb_io,
+                                                         uint64_t* __restrict__ starts) {
     FeView f{x, cost, fc, summ, n, nc, uniform64(fc[nc])};
-    const uint64_t nb = *nb_in;
+    const uint64_t nb = nb_io[0];
     const uint64_t k = (uint64_t)blockIdx.x * 4 + wave_id();
-    if (k == 0 && lane_id() == 0) {
-        starts[0] = 0;
-        starts[nb] = n;
-    }
-    if (k + 1 >= nb) return;
+    if (k == 0 && lane_id() == 0) starts[0] = entry & ~(1ull << 63);
+    if (k >= nb) return;
     const uint64_t b = bnd[k];
     uint64_t pos;
     if (b >> 63) pos = b & ~(1ull << 63);
     else pos = ginv(f, b);
-    if (lane_id() == 0) starts[k + 1] = pos;
+    if (lane_id() == 0) {
+        starts[k + 1] = pos;
+        if (k + 1 == nb) {
+            const bool mid = pos > 0 && pos < n && x[pos] == x[pos - 1];
+            nb_io[2] = (pos >= n_own ? pos - n_own : 0) | (mid ? 1ull << 63 : 0);
+        }
+    }
 }
 
 namespace {

@@ -127,12 +127,15 @@ __global__ void fe_costscan_kernel(const uint32_t* ccost, uint64_t nc, uint64_t*
 __global__ void fe_dmap_kernel(const uint8_t* x, const uint8_t* cost, uint64_t n, uint64_t nc, const uint64_t* fc,
                                uint8_t* dmap);
 constexpr int kFeChainThreads = 1024;  // one workgroup
+// chain of one unit of the stream (own bytes [0, n_own), tail halo up to n),
+// first block at `entry` (bit 63: mid-run); out[0] blocks, out[1] status
 __global__ void fe_chain_kernel(const uint8_t* x, const uint8_t* cost, const uint64_t* fc, const uint4* summ,
-                                const uint8_t* dmap, uint64_t n, uint64_t nc, int S, uint64_t* bnd, uint64_t max_bnd,
-                                uint64_t* nb_out);
+                                const uint8_t* dmap, uint64_t n, uint64_t nc, int S, uint64_t n_own, uint64_t entry,
+                                int ends, uint64_t* bnd, uint64_t max_bnd, uint64_t* out);
+// starts[0..nb] from the chain; nb_io[2] = exit token of the next unit
 __global__ void fe_resolve_kernel(const uint8_t* x, const uint8_t* cost, const uint64_t* fc, const uint4* summ,
-                                  uint64_t n, uint64_t nc, const uint64_t* bnd, const uint64_t* nb_in,
-                                  uint64_t* starts);
+                                  uint64_t n, uint64_t nc, uint64_t n_own, uint64_t entry, const uint64_t* bnd,
+                                  uint64_t* nb_io, uint64_t* starts);
 __global__ void fe_rle1_kernel(const uint8_t* x, uint64_t n, const uint64_t* starts, uint64_t first, uint64_t count,
                                uint8_t* blocks, size_t stride, uint32_t* lens);
 __global__ void fe_crc_kernel(const uint8_t* x, uint64_t n, const uint64_t* starts, uint64_t first, uint64_t count,

@@ -119,6 +119,65 @@ int bz2mi_last_stats(bz2mi_ctx* ctx, uint64_t* out8);
 /* Number of blocks compressed so far in this stream. */
 uint64_t bz2mi_blocks_done(const bz2mi_ctx* ctx);
 
+/* ---- one logical stream compressed in units ------
+ * The reference compresses one stream on one device: OutputStream feeds the
+ * blocks in order (OutputStream.hpp:131-142, 179-188), the per-slot frequency
+ * array persists across batches (OutputStream.hpp:93, kernel.cpp:3155) and the
+ * block bits are stitched and the stream CRC chained in block order
+ * (OutputStream.hpp:190-240, :202).  Here the stream is cut into units --
+ * contiguous byte ranges, each compressed by a context on any device or process
+ * -- and the output is the same stream, bit for bit.  Per unit, in order:
+ *
+ *   begin     the unit's bytes [0, n_own) plus a tail halo [n_own, n_own+n_halo)
+ *             (the bytes that follow it in the stream, bz2mi_unit_halo() of
+ *             them, or up to the stream end: BZ2MI_UNIT_ENDS_STREAM) are in HBM;
+ *             the data-parallel front end starts (asynchronous).
+ *   chain     the unit's blocks (the RLE1 block split, OutputStream.hpp:179-188):
+ *             `entry` = where its first block starts, from the previous unit's
+ *             exit (the first unit: 0); returns the next unit's entry and the
+ *             block count.  Block indices continue from `first_block` (the sum
+ *             of the earlier units' counts).  Synchronous; then RLE1, CRC, BWT,
+ *             MTF/RLE2 run asynchronously.
+ *   sums      the unit's per-slot symbol histogram sums (p x 258 uint32, slot =
+ *             stream block index mod p): its share of the persistent frequency
+ *             array.
+ *   encode    `carried` = the uint32 sum of the sums of every earlier unit:
+ *             Huffman tables and block payloads; returns the unit's bits (81
+ *             header bits + payload per block) and its CRC share
+ *             XOR_b rotl(crc_b, m-1-b) over its m blocks.
+ *   assemble  the unit's bytes for a stream bit offset: the first byte's top
+ *             (bit_offset & 7) bits are zero (OR it into the previous unit's
+ *             last byte); BZ2MI_UNIT_FIRST prepends "BZh<level>" (bit_offset
+ *             0), BZ2MI_UNIT_LAST appends the end-of-stream marker with the
+ *             stream CRC rotl(crc_before, m) ^ share and pads to a byte.
+ * A unit whose entry lies at or past n_own has no blocks: chain returns
+ * nblocks = 0 and exit = entry - n_own, and it takes no further part.
+ * bz2mi_shard (bzip2-opencl_amd/bz2mi/shard.py) drives this protocol across
+ * ranks with torch.distributed; a context runs its units' BWTs one at a time.
+ */
+typedef struct bz2mi_unit bz2mi_unit;
+#define BZ2MI_UNIT_ENDS_STREAM 1 /* begin: the halo reaches the end of the stream */
+#define BZ2MI_UNIT_FIRST 1       /* assemble: stream header first */
+#define BZ2MI_UNIT_LAST 2        /* assemble: end-of-stream trailer last */
+#define BZ2MI_ENTRY_MIDRUN (1ull << 63) /* entry/exit flag: x[p] == x[p-1] in the stream */
+
+/* tail halo bytes a unit needs (the longest raw span of one block) */
+size_t bz2mi_unit_halo(int level, int unit);
+bz2mi_unit* bz2mi_unit_create(bz2mi_ctx* ctx);
+void bz2mi_unit_destroy(bz2mi_unit* u);
+/* d_buf: device bytes (n_own + n_halo), read until the unit is assembled;
+ * hip_stream: the stream that wrote them (NULL: the null stream) */
+int bz2mi_unit_begin(bz2mi_unit* u, const void* d_buf, size_t n_own, size_t n_halo, int flags, void* hip_stream);
+int bz2mi_unit_chain(bz2mi_unit* u, uint64_t entry, uint64_t first_block, uint64_t* exit_entry, uint64_t* nblocks);
+int bz2mi_unit_sums(bz2mi_unit* u, uint32_t* sums);
+int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, uint32_t* crc);
+/* d_out: device memory, 4-byte aligned, >= (bits + 7 + 32 + 80) / 8 + 4 bytes */
+int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags, void* d_out, size_t cap,
+                        size_t* out_bytes);
+/* milliseconds of the unit's stages (HIP events): front scan, chain (host wall),
+ * RLE1 + CRC + BWT, MTF, Huffman, assembly */
+int bz2mi_unit_timings(bz2mi_unit* u, float* ms6);
+
 /* ---- decompression on the device ----------
  * Replaces the reference's InputStream (InputStream.hpp:36-159),
  * BlockDecompressor (BlockDecompressor.hpp:37-282) and HuffmanStageDecoder

@@ -726,3 +726,197 @@ long long cpuref_compress(const uint8_t* in, size_t n, int level, int p, int uni
     pthread_mutex_destroy(&j.mu);
     return ret;
 }
+
+/* ---------------------------------------------------------- stream units --
+ * The block chain from `entry` (a block start: the RLE1 state restarts there,
+ * BlockCompressor.hpp:120-131) until the next start lies at or past n_own;
+ * blocks then go through the same stages as cpuref_compress, with stream block
+ * indices first_block.. for the seed slots (H4) and the stream CRC / bit
+ * offsets supplied by the caller (OutputStream.hpp:190-240, :202). */
+struct cpuref_unit {
+    int level, p, S;
+    long long nb;
+    uint64_t first_block;
+    uint32_t* crcs;
+    job_t j;
+    uint32_t* seeds;
+};
+
+#define UNIT_MIDRUN (1ull << 63)
+
+cpuref_unit* cpuref_unit_open(const uint8_t* buf, size_t n_own, size_t n_halo, int ends, int level, int p,
+                              int unit, uint64_t entry, uint64_t first_block, uint64_t* exit_entry,
+                              uint64_t* nblocks, int threads) {
+    if (level < 1 || level > 9 || p < 1 || unit < 10 || n_own == 0 || !exit_entry || !nblocks) return NULL;
+    const int S = unit * level;
+    const size_t n = n_own + n_halo;
+    cpuref_unit* u = (cpuref_unit*)calloc(1, sizeof(cpuref_unit));
+    u->level = level;
+    u->p = p;
+    u->S = S;
+    u->first_block = first_block;
+    size_t pos = (size_t)(entry & ~UNIT_MIDRUN);
+    /* pass 1: count the blocks; pass 2: emit them */
+    size_t cap = (n_own + n_own / 4) / (size_t)(S - 5) + 4;
+    size_t stride = (size_t)S + 8;
+    uint8_t* blocks = (uint8_t*)malloc(cap * stride + 1);
+    uint64_t* starts = (uint64_t*)malloc(sizeof(uint64_t) * (cap + 1));
+    uint32_t* lens = (uint32_t*)malloc(sizeof(uint32_t) * (cap + 1));
+    u->crcs = (uint32_t*)malloc(sizeof(uint32_t) * (cap + 1));
+    long long nb = 0;
+    int bad = 0;
+    while (pos < n_own) {
+        if ((size_t)nb >= cap) {
+            bad = 1;
+            break;
+        }
+        rle1_state s;
+        s.blk = blocks + nb * stride;
+        s.len = 0;
+        s.limit = S - 6;
+        s.run = 0;
+        s.val = -1;
+        size_t i = pos;
+        while (i < n && rle1_put(&s, buf[i])) ++i;
+        if (i >= n && !ends) {
+            bad = 1; /* the block runs past the halo */
+            break;
+        }
+        if (s.run > 0) rle1_flush(&s, s.val & 0xff, s.run);
+        starts[nb] = pos;
+        lens[nb] = (uint32_t)s.len;
+        u->crcs[nb] = ~cpuref_crc_update(0xffffffffu, buf + pos, i - pos);
+        nb++;
+        pos = i;
+    }
+    if (bad) {
+        free(blocks);
+        free(starts);
+        free(lens);
+        free(u->crcs);
+        free(u);
+        return NULL;
+    }
+    if (pos >= n_own) {
+        const int mid = pos > 0 && pos < n && buf[pos] == buf[pos - 1];
+        *exit_entry = (uint64_t)(pos - n_own) | (mid ? UNIT_MIDRUN : 0);
+    }
+    if (nb == 0) *exit_entry = ((entry & ~UNIT_MIDRUN) - n_own) | (entry & UNIT_MIDRUN);
+    *nblocks = (uint64_t)nb;
+    u->nb = nb;
+    job_t* j = &u->j;
+    memset(j, 0, sizeof(*j));
+    pthread_mutex_init(&j->mu, NULL);
+    j->in = buf;
+    j->starts = starts;
+    j->lens = lens;
+    j->blocks = blocks;
+    j->stride = stride;
+    j->nb = nb;
+    j->bwt = (uint8_t*)malloc(nb * stride + 1);
+    j->mtf = (uint16_t*)malloc(sizeof(uint16_t) * nb * (stride + 2) + 2);
+    j->hist = (uint32_t*)malloc(sizeof(uint32_t) * 258 * (nb + 1));
+    j->mtflen = (int*)malloc(sizeof(int) * (nb + 1));
+    j->alpha = (int*)malloc(sizeof(int) * (nb + 1));
+    j->orig = (int*)malloc(sizeof(int) * (nb + 1));
+    j->present = (uint8_t*)malloc(256 * (nb + 1));
+    j->phase = 0;
+    if (nb) run_pool(j, threads);
+    return u;
+}
+
+void cpuref_unit_sums(const cpuref_unit* u, uint32_t* sums) {
+    memset(sums, 0, sizeof(uint32_t) * 258 * (size_t)u->p);
+    for (long long b = 0; b < u->nb; ++b) {
+        const int slot = (int)((u->first_block + (uint64_t)b) % (uint64_t)u->p);
+        for (int s = 0; s < 258; ++s) sums[slot * 258 + s] += u->j.hist[b * 258 + s];
+    }
+}
+
+int cpuref_unit_encode(cpuref_unit* u, const uint32_t* carried, uint64_t* bits, uint32_t* crc, int threads) {
+    const long long nb = u->nb;
+    job_t* j = &u->j;
+    free(u->seeds);
+    u->seeds = (uint32_t*)malloc(sizeof(uint32_t) * 258 * (nb + 1));
+    uint32_t* acc = (uint32_t*)malloc(sizeof(uint32_t) * 258 * (size_t)u->p);
+    memcpy(acc, carried, sizeof(uint32_t) * 258 * (size_t)u->p);
+    for (long long b = 0; b < nb; ++b) {
+        const int slot = (int)((u->first_block + (uint64_t)b) % (uint64_t)u->p);
+        for (int s = 0; s < 258; ++s) {
+            acc[slot * 258 + s] += j->hist[b * 258 + s];
+            u->seeds[b * 258 + s] = acc[slot * 258 + s];
+        }
+    }
+    free(acc);
+    j->seeds = u->seeds;
+    j->payload_stride = (size_t)u->S * 20 / 8 + u->S / 50 + 8 * 1024;
+    free(j->payload);
+    free(j->pbits);
+    j->payload = (uint8_t*)malloc(j->payload_stride * nb + 1);
+    j->pbits = (long long*)malloc(sizeof(long long) * (nb + 1));
+    j->phase = 1;
+    if (nb) run_pool(j, threads);
+    uint64_t tot = 0;
+    uint32_t x = 0;
+    for (long long b = 0; b < nb; ++b) {
+        if (j->pbits[b] < 0) return -2;
+        tot += 81 + (uint64_t)j->pbits[b];
+        const uint32_t r = (uint32_t)(nb - 1 - b) & 31u;
+        x ^= r ? (u->crcs[b] << r) | (u->crcs[b] >> (32 - r)) : u->crcs[b];
+    }
+    *bits = tot;
+    *crc = x;
+    return 0;
+}
+
+long long cpuref_unit_assemble(const cpuref_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags,
+                               uint8_t* out, size_t cap) {
+    const job_t* j = &u->j;
+    bitw w = {out, 0, (uint64_t)cap * 8, 0};
+    if (flags & 1) {
+        bw_bits(&w, 16, 0x425a);
+        bw_bits(&w, 8, 0x68);
+        bw_bits(&w, 8, (uint32_t)('0' + u->level));
+    } else {
+        for (uint64_t k = 0; k < (bit_offset & 7); ++k) bw_bit(&w, 0);
+    }
+    uint32_t streamCRC = crc_before;
+    for (long long b = 0; b < u->nb; ++b) {
+        streamCRC = ((streamCRC << 1) | (streamCRC >> 31)) ^ u->crcs[b];
+        bw_bits(&w, 24, 0x314159);
+        bw_bits(&w, 24, 0x265359);
+        bw_int(&w, u->crcs[b]);
+        bw_bit(&w, 0);
+        put_bits_from(&w, j->payload + b * j->payload_stride, (uint64_t)j->pbits[b]);
+    }
+    if (flags & 2) {
+        bw_bits(&w, 24, 0x177245);
+        bw_bits(&w, 24, 0x385090);
+        bw_int(&w, streamCRC);
+    }
+    const uint64_t nbits = w.n;
+    while (w.n & 7) bw_bit(&w, 0);
+    if (w.overflow) return -2;
+    return (long long)((nbits + 7) >> 3);
+}
+
+void cpuref_unit_free(cpuref_unit* u) {
+    if (!u) return;
+    job_t* j = &u->j;
+    free((void*)j->starts);
+    free((void*)j->lens);
+    free(j->blocks);
+    free(j->bwt);
+    free(j->mtf);
+    free(j->hist);
+    free(j->mtflen);
+    free(j->alpha);
+    free(j->orig);
+    free(j->present);
+    free(j->payload);
+    free(j->pbits);
+    free(u->seeds);
+    free(u->crcs);
+    pthread_mutex_destroy(&j->mu);
+    free(u);
+}

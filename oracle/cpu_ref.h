@@ -61,6 +61,25 @@ long long cpuref_block_payload(int origPtr, const uint8_t* present, const uint16
 long long cpuref_compress(const uint8_t* in, size_t n, int level, int p, int unit, uint8_t* out,
                           size_t cap, int threads);
 
+/* ---- stream units: the protocol of include/bz2mi.h's
+ *      bz2mi_unit_* restated on the host (same arguments, same results), so
+ *      the distributed driver (bz2mi/shard.py) can be checked on CPU ranks.
+ *      open = begin + chain (and RLE1/BWT/MTF): buf holds n_own bytes plus an
+ *      n_halo tail halo (ends: it reaches the stream end); entry / exit as in
+ *      bz2mi_unit_chain.  Returns NULL on bad arguments or a halo too short. */
+typedef struct cpuref_unit cpuref_unit;
+cpuref_unit* cpuref_unit_open(const uint8_t* buf, size_t n_own, size_t n_halo, int ends, int level, int p,
+                              int unit, uint64_t entry, uint64_t first_block, uint64_t* exit_entry,
+                              uint64_t* nblocks, int threads);
+void cpuref_unit_sums(const cpuref_unit* u, uint32_t* sums);
+int cpuref_unit_encode(cpuref_unit* u, const uint32_t* carried, uint64_t* bits, uint32_t* crc, int threads);
+/* flags: 1 = stream header first, 2 = end-of-stream trailer last; returns the
+ * byte count (the first byte's top bit_offset&7 bits are zero), -2 if cap is
+ * too small */
+long long cpuref_unit_assemble(const cpuref_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags,
+                               uint8_t* out, size_t cap);
+void cpuref_unit_free(cpuref_unit* u);
+
 /* Upper bound of the compressed size for cpuref_compress / the product. */
 size_t cpuref_bound(size_t n, int level, int unit);
 

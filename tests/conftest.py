@@ -103,6 +103,79 @@ def cpuref():
     return CpuRef()
 
 
+class CpuRefUnit:
+    """The unit protocol (include/bz2mi.h bz2mi_unit_*) on the C restatement
+    (cpuref_unit_*), for driving bz2mi.shard on CPU ranks."""
+
+    def __init__(self, level=9, parallel=10, unit=10000, threads=2):
+        self.L = CpuRef().L
+        c = ctypes
+        L = self.L
+        L.cpuref_unit_open.restype = c.c_void_p
+        L.cpuref_unit_open.argtypes = [c.c_char_p, c.c_size_t, c.c_size_t, c.c_int, c.c_int, c.c_int, c.c_int,
+                                       c.c_uint64, c.c_uint64, c.POINTER(c.c_uint64), c.POINTER(c.c_uint64), c.c_int]
+        L.cpuref_unit_sums.argtypes = [c.c_void_p, c.c_void_p]
+        L.cpuref_unit_encode.restype = c.c_int
+        L.cpuref_unit_encode.argtypes = [c.c_void_p, c.c_void_p, c.POINTER(c.c_uint64), c.POINTER(c.c_uint32),
+                                         c.c_int]
+        L.cpuref_unit_assemble.restype = c.c_longlong
+        L.cpuref_unit_assemble.argtypes = [c.c_void_p, c.c_uint64, c.c_uint32, c.c_int, c.c_char_p, c.c_size_t]
+        L.cpuref_unit_free.argtypes = [c.c_void_p]
+        self.level, self.parallel, self.unit, self.threads = level, parallel, unit, threads
+        self.h = None
+
+    def begin(self, buf: bytes, n_own: int, n_halo: int, ends: bool):
+        self.buf = bytes(buf)
+        self.n_own, self.n_halo, self.ends = n_own, n_halo, ends
+
+    def chain(self, entry, first_block):
+        ex = ctypes.c_uint64(0)
+        nb = ctypes.c_uint64(0)
+        self.h = self.L.cpuref_unit_open(self.buf, self.n_own, self.n_halo, 1 if self.ends else 0, self.level,
+                                         self.parallel, self.unit, entry, first_block, ctypes.byref(ex),
+                                         ctypes.byref(nb), self.threads)
+        assert self.h, "cpuref_unit_open failed (halo too short?)"
+        return ex.value, nb.value
+
+    def sums(self):
+        import numpy as np
+        out = np.zeros(self.parallel * 258, dtype=np.uint32)
+        self.L.cpuref_unit_sums(self.h, out.ctypes.data)
+        return out
+
+    def encode(self, carried):
+        import numpy as np
+        c = np.ascontiguousarray(carried, dtype=np.uint32)
+        bits = ctypes.c_uint64(0)
+        crc = ctypes.c_uint32(0)
+        assert self.L.cpuref_unit_encode(self.h, c.ctypes.data, ctypes.byref(bits), ctypes.byref(crc),
+                                         self.threads) == 0
+        self.bits = bits.value
+        return bits.value, crc.value
+
+    def assemble(self, bit_offset, crc_before, flags):
+        cap = (self.bits + 32 + 80) // 8 + 16
+        out = ctypes.create_string_buffer(cap)
+        n = self.L.cpuref_unit_assemble(self.h, bit_offset, crc_before, flags, out, cap)
+        assert n >= 0
+        return out.raw[:n]
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.cpuref_unit_free(self.h)
+            self.h = None
+
+
+def unit_buffers(data: bytes, cuts: list[int], halo: int):
+    """Split a stream at `cuts` into unit buffers: (bytes own+halo, n_own, n_halo, ends)."""
+    bounds = [0] + list(cuts) + [len(data)]
+    out = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        end = min(len(data), b + halo)
+        out.append((data[a:end], b - a, end - b, end == len(data)))
+    return out
+
+
 def oref_lib():
     path = os.path.join(REPO, "oracle", "_ref", "liboref.so")
     if not os.path.exists(path):

@@ -1,0 +1,202 @@
+"""One logical stream compressed in units: the unit
+protocol of include/bz2mi.h driven by bz2mi.shard must give the bytes of the
+single-device stream for the concatenated input (OutputStream.hpp:131-240).
+
+CPU tests run the protocol on the C restatement's units (cpuref_unit_*) in one
+process and across two gloo ranks; the `gpu` tests run the device units
+(bz2mi_unit_*) in one process and in two processes sharing cuda:0."""
+from __future__ import annotations
+
+import bz2
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import CpuRef, CpuRefUnit, have_gpu, unit_buffers
+
+import bz2mi
+from bz2mi import shard, synth
+
+
+def _stream_case(n: int, seed: int) -> bytes:
+    """Mixed data with every boundary hazard: random, text, long runs (a 300 KB
+    run spans several -1 blocks, runs of 4..300 cut RLE1 pieces), ACGT."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    parts = [synth.random_bytes(n // 5, seed), synth.text_bytes(n // 5, seed + 1),
+             np.full(300_000, 0x41, dtype=np.uint8), synth.runs_bytes(n // 5, seed + 2),
+             synth.small_alphabet_bytes(n // 5, seed + 3), np.full(777, 7, dtype=np.uint8),
+             rng.integers(0, 256, size=n // 10, dtype=np.uint8)]
+    return np.concatenate(parts).tobytes()
+
+
+def _cuts(n: int, seed: int, k: int, S: int) -> list[int]:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cuts = sorted(set(int(v) for v in rng.integers(1, n - 1, size=k)))
+    # a few adversarial ones: tiny units (inside one block), cuts inside the long run
+    extra = [cuts[0] + 1, cuts[0] + 3, n // 5 * 2 + 100_000, n // 5 * 2 + 100_255, n - 2]
+    return sorted(set(c for c in cuts + extra if 0 < c < n))
+
+
+def run_units(data: bytes, cuts: list[int], level: int, p: int, unit: int = 10000) -> bytes:
+    halo = bz2mi.unit_halo(level, unit)
+    units = {}
+    for g, (buf, n_own, n_halo, ends) in enumerate(unit_buffers(data, cuts, halo)):
+        u = CpuRefUnit(level, p, unit)
+        u.begin(buf, n_own, n_halo, ends)
+        units[g] = u
+    lay = shard.compress_units(units, [0] * len(units), p, level)
+    return shard.gather_stream_host(lay, level)
+
+
+@pytest.mark.parametrize("level,p", [(1, 10), (1, 3), (2, 1), (9, 10)])
+def test_units_one_process_equal_single_stream(level, p):
+    data = _stream_case(1_200_000, 0x5EED0101 + level)
+    want = CpuRef().compress(data, level, p)
+    got = run_units(data, _cuts(len(data), 7 * level + p, 6, level * 10000), level, p)
+    assert got == want
+    assert bz2.decompress(got) == data
+
+
+def test_units_edge_layouts():
+    data = _stream_case(400_000, 0x5EED0202)
+    want = CpuRef().compress(data, 1, 10)
+    for cuts in ([], [1], [len(data) - 1], list(range(1000, len(data), 37_000)),
+                 [5, 6, 7, 8, 9, 10]):
+        assert run_units(data, cuts, 1, 10) == want, cuts
+    # the whole stream one long run: every unit but the first covered by others
+    run = bytes(2_000_000)
+    assert run_units(run, [100, 200_000, 1_000_000], 1, 10) == CpuRef().compress(run, 1, 10)
+    # empty stream
+    assert shard.empty_stream(9) == CpuRef().compress(b"", 9, 10)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cpu_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data = _stream_case(1_500_000, 0x5EED0303)
+    cuts = _cuts(len(data), 11, 9, 10000)
+    halo = bz2mi.unit_halo(1, 10000)
+    bufs = unit_buffers(data, cuts, halo)
+    owners = shard.interleaved_owners(len(bufs), world)
+    units = {}
+    for g, (buf, n_own, n_halo, ends) in enumerate(bufs):
+        if owners[g] == rank:
+            u = CpuRefUnit(1, 10, 10000)
+            u.begin(buf, n_own, n_halo, ends)
+            units[g] = u
+    lay = shard.compress_units(units, owners, 10, 1)
+    got = shard.gather_stream_host(lay, 1)
+    if rank == 0:
+        q.put(got == CpuRef().compress(data, 1, 10))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_two_ranks_one_stream():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert ok
+    assert all(p.exitcode == 0 for p in procs)
+
+
+# ---------------------------------------------------------------- device ----
+
+def _device_units(ctx, data_t: torch.Tensor, cuts: list[int], owners, rank, level, unit=10000):
+    halo = bz2mi.unit_halo(level, unit)
+    n = data_t.numel()
+    bounds = [0] + list(cuts) + [n]
+    units = {}
+    for g, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
+        if owners[g] != rank:
+            continue
+        end = min(n, b + halo)
+        buf = data_t[a:end].clone()  # a unit's own buffer (bytes + halo), as a rank would hold it
+        u = shard.DeviceUnit(ctx, data_t.device)
+        u.begin(buf, b - a, end - b, end == n)
+        units[g] = u
+    return units
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not have_gpu(), reason="needs a HIP device")
+@pytest.mark.parametrize("level,p,n", [(9, 10, 24 << 20), (1, 10, 3 << 20), (1, 3, 2 << 20)])
+def test_device_units_equal_single_stream(level, p, n):
+    data = _stream_case(n, 0x5EED0404 + level)
+    dev = torch.device("cuda", 0)
+    x = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    ctx = bz2mi.Context(level, p, 10000)
+    cuts = _cuts(len(data), 3 + level, 5, level * 10000)
+    owners = [0] * (len(cuts) + 1)
+    units = _device_units(ctx, x, cuts, owners, 0, level)
+    lay = shard.compress_units(units, owners, p, level)
+    out = torch.empty(lay.stream_bytes + 64, dtype=torch.uint8, device=dev)
+    got = shard.gather_stream_device(lay, shard.settle(lay), out, level).cpu().numpy().tobytes()
+    cap = bz2mi.compress_bound(len(data), level, 10000)
+    o2 = torch.empty(cap, dtype=torch.uint8, device=dev)
+    m = ctx.compress_device(x.data_ptr(), len(data), o2.data_ptr(), cap)
+    whole = o2[:m].cpu().numpy().tobytes()
+    assert got == whole
+    assert whole == CpuRef().compress(data, level, p)
+
+
+def _gpu_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    data = synth.mixed_bytes(16 << 20, synth.SEED_MIXED, segment=1 << 20).tobytes()
+    x = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    ctx = bz2mi.Context(9, 10, 10000)
+    cuts = [(16 << 20) * k // 6 for k in range(1, 6)]
+    owners = shard.interleaved_owners(len(cuts) + 1, world)
+    units = _device_units(ctx, x, cuts, owners, rank, 9)
+    lay = shard.compress_units(units, owners, 10, 9)
+    # device pieces -> host bytes, gathered over gloo (both ranks share one GPU)
+    for g in list(lay.pieces):
+        t, nb = lay.pieces[g]
+        lay.pieces[g] = t[:nb].cpu().numpy().tobytes()
+    got = shard.gather_stream_host(lay, 9)
+    if rank == 0:
+        q.put((got == bz2mi.compress(data, 9, 10), got == CpuRef().compress(data, 9, 10),
+               bz2.decompress(got) == data))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not have_gpu(), reason="needs a HIP device")
+@pytest.mark.timeout(600)
+def test_device_two_ranks_one_stream():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=500)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == (True, True, True)
+    assert all(p.exitcode == 0 for p in procs)
