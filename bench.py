@@ -149,6 +149,37 @@ def cpu_baseline(sample_bytes: int) -> dict:
     return res
 
 
+def reference_gpu(sample_bytes: int) -> dict | None:
+    """The reference itself on this GPU: its app.cpp + kernel.cpp, unmodified
+    (oracle/_ref/ref_app, built from /root/reference), compressing a file of
+    random bytes through the ROCm OpenCL runtime at -9 with its thesis setting
+    p = 1024 (default p = 10 leaves 10 lanes busy).  Process wall time.
+    Its Huffman tables differ from O_ref's (hazard H3, tests/test_refgpu.py);
+    the stream is checked to decode."""
+    import bz2
+    import tempfile
+    from bz2mi import synth
+    app = os.path.join(REPO, "oracle", "_ref", "ref_app")
+    if not os.path.exists(app):
+        return None
+    data = synth.random_bytes(sample_bytes, 0x5EED2002).tobytes()
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        f = os.path.join(d, "in.bin")
+        with open(f, "wb") as h:
+            h.write(data)
+        t0 = time.perf_counter()
+        r = subprocess.run([app, f, "-k", "-s", "9", "-p", "1024"], capture_output=True, timeout=300)
+        dt = time.perf_counter() - t0
+        if r.returncode != 0:
+            return None
+        with open(f + ".bz2", "rb") as h:
+            z = h.read()
+    ok = bz2.decompress(z) == data
+    return {"value": round(len(data) / dt / 1e6, 3), "unit": "MB/s", "seconds": round(dt, 2),
+            "sample": f"{len(data) >> 20} MiB random bytes, app.cpp -s 9 -p 1024 (file -> file, OpenCL on this GPU)",
+            "decodes": ok}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,9 +192,10 @@ def main():
     ap.add_argument("--cpu-sample-mib", type=int, default=96)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--mode", choices=["compress", "decompress"], default="compress",
+    ap.add_argument("--mode", choices=["compress", "decompress", "e2e"], default="compress",
                     help="compress = the bench line (BASELINE metric); decompress = configs[4]: device "
-                         "decompression of the stream this run compresses (output MB/s)")
+                         "decompression of the stream this run compresses (output MB/s); e2e = file -> file "
+                         "through the reference's unmodified app.cpp built against the mirror headers")
     ap.add_argument("--data", choices=["random", "text", "mixed"], default="random",
                     help="random = C2 (the bench line); text = C3 stand-in (seeded word Markov text, enwik9 is "
                          "not available offline); mixed = C4 (rotating random/text/runs/ACGT segments)")
@@ -219,6 +251,8 @@ def main():
 
     if args.mode == "decompress":
         return bench_decompress(args, ctx, x, n, out, cap, world, rank, dev)
+    if args.mode == "e2e":
+        return bench_e2e(args, ctx, x, n, out, cap)
 
     for _ in range(args.warmup):
         out_len = step()
@@ -283,6 +317,7 @@ def main():
             "pipeline_GBps": round((n + out_len) / (ms_step * 1e-3) / 1e9, 2),
             "stage_ms": {k: round(v, 3) for k, v in avg.items()}}
     cpu = None if args.no_cpu else cpu_baseline(args.cpu_sample_mib << 20)
+    refgpu = None if args.no_cpu else reference_gpu(64 << 20)
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
@@ -293,6 +328,7 @@ def main():
                    "blocks": nb, "parallelism": f"dp{world} (independent streams)", "decode_check": verified},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "reference_on_this_gpu": refgpu,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
@@ -451,6 +487,49 @@ def bench_units(args, world: int):
 
 WORKLOAD_DATA = {"random": "random bytes, unit g seeded 0x5EED0001+g", "text": "word-Markov text, unit g seeded "
                  "0x5EED0002+g", "mixed": "C4 mixed-entropy segments, seed 0x5EED0003"}
+
+
+def bench_e2e(args, ctx, x, n, out, cap):
+    """End to end, SURVEY.md section 8(d): the reference's app.cpp, unmodified,
+    compiled against the mirror OutputStream (raw bytes to the device front end
+    in 64 MiB stream units, pinned double buffers), file -> file on the local
+    disk: `app_bz2mi <file> -k -s <level> -p <p>`, wall time of the process
+    (process start, HIP init, read, compress, write).  The file is checked
+    against the device-path stream of the same bytes."""
+    import hashlib
+    import tempfile
+    app = os.path.join(PKG, "build", "app_bz2mi")
+    if not os.path.exists(app):
+        raise SystemExit("app_bz2mi not built (__graft_entry__.build() in the build container)")
+    m = ctx.compress_device(x.data_ptr(), n, out.data_ptr(), cap)
+    want = hashlib.sha256(out[:m].cpu().numpy().tobytes()).hexdigest()
+    host = x.cpu().numpy().tobytes()
+    times = []
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        src = os.path.join(d, "in.bin")
+        with open(src, "wb") as f:
+            f.write(host)
+        del host
+        same = None
+        for i in range(args.warmup + args.steps):
+            t0 = time.perf_counter()
+            subprocess.run([app, src, "-k", "-s", str(args.level), "-p", str(args.parallel)], check=True)
+            dt = time.perf_counter() - t0
+            with open(src + ".bz2", "rb") as f:
+                got = hashlib.sha256(f.read()).hexdigest()
+            same = (same is not False) and got == want
+            os.unlink(src + ".bz2")
+            if i >= args.warmup:
+                times.append(dt)
+    t = sum(times) / len(times)
+    line = {"metric": "end-to-end compress MB/s (file -> file, unmodified app.cpp on the mirror headers)",
+            "value": round(n / t / 1e6, 2), "unit": "MB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic",
+            "config": {"workload": WORKLOADS[args.data].format(mib=args.mib) + " written to a local file",
+                       "level": args.level, "parallel_blocks": args.parallel, "unit_bytes": 64 << 20,
+                       "same_bytes_as_device_path": bool(same), "seconds": [round(v, 3) for v in times]}}
+    print(json.dumps(line), flush=True)
 
 
 def bench_decompress(args, ctx, x, n, out, cap, world, rank, dev):

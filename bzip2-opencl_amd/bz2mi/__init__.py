@@ -34,6 +34,7 @@ EXPORTS = (
     "bz2mi_last_stats", "bz2mi_dcreate", "bz2mi_ddestroy", "bz2mi_decompress", "bz2mi_decompress_device",
     "bz2mi_dlast_timings", "bz2mi_unit_halo", "bz2mi_unit_create", "bz2mi_unit_destroy", "bz2mi_unit_begin",
     "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode", "bz2mi_unit_assemble", "bz2mi_unit_timings",
+    "bz2mi_host_alloc", "bz2mi_host_free", "bz2mi_unit_begin_host", "bz2mi_unit_assemble_host",
 )
 
 _lib = None

@@ -48,6 +48,10 @@ struct bz2mi_unit {
     float chain_ms = 0;
     hipEvent_t ev_in = nullptr;
     hipEvent_t ev[12] = {};  // stage brackets: front, rle1+bwt, mtf, (seed), huffman, assembly
+    uint8_t* d_own = nullptr;  // host-fed units: device copy of the bytes
+    size_t own_cap = 0;
+    uint8_t* d_out = nullptr;  // host-fed units: assembled bytes
+    size_t out_cap = 0;
 };
 
 namespace {
@@ -94,6 +98,8 @@ void bz2mi_unit_destroy(bz2mi_unit* u) {
         if (st) (void)hipStreamSynchronize(st);
     free_front(u->fe);
     free_batch(u->t);
+    if (u->d_own) (void)hipFree(u->d_own);
+    if (u->d_out) (void)hipFree(u->d_out);
     if (u->d_state) (void)hipFree(u->d_state);
     if (u->d_sd) (void)hipFree(u->d_sd);
     if (u->ev_in) (void)hipEventDestroy(u->ev_in);
@@ -261,6 +267,53 @@ int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before,
     HIPCHECK(hipEventRecord(u->ev[10], s));
     HIPCHECK(hipStreamSynchronize(s));
     *out_bytes = (size_t)nbytes;
+    return BZ2MI_OK;
+}
+
+void* bz2mi_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        fail(BZ2MI_EDEVICE, "hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void bz2mi_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int bz2mi_unit_begin_host(bz2mi_unit* u, const void* host, size_t n_own, size_t n_halo, int flags) {
+    if (!u || (!host && n_own + n_halo)) return fail(BZ2MI_EINVAL, "null argument");
+    bz2mi_ctx* c = u->c;
+    HIPCHECK(hipSetDevice(c->device));
+    const size_t n = n_own + n_halo;
+    if (n + 64 > u->own_cap) {
+        int r;
+        const size_t cap = n + n / 8 + 64;
+        if ((r = dalloc(&u->d_own, cap))) return r;
+        u->own_cap = cap;
+    }
+    // on the front-scan stream: begin() orders the scan after it
+    HIPCHECK(hipMemcpyAsync(u->d_own, host, n, hipMemcpyHostToDevice, c->sF));
+    return bz2mi_unit_begin(u, u->d_own, n_own, n_halo, flags, c->sF);
+}
+
+int bz2mi_unit_assemble_host(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags, void* host_out,
+                             size_t cap, size_t* out_bytes) {
+    if (!u || !host_out || !out_bytes) return fail(BZ2MI_EINVAL, "null argument");
+    bz2mi_ctx* c = u->c;
+    HIPCHECK(hipSetDevice(c->device));
+    const size_t need = (size_t)((u->bits + 32 + 80 + 7) / 8) + 64;
+    if (need > u->out_cap) {
+        int r;
+        if ((r = dalloc(&u->d_out, need + need / 8))) return r;
+        u->out_cap = need + need / 8;
+    }
+    int r = bz2mi_unit_assemble(u, bit_offset, crc_before, flags, u->d_out, u->out_cap, out_bytes);
+    if (r) return r;
+    if (*out_bytes > cap) return fail(BZ2MI_ESPACE, "output buffer too small");
+    HIPCHECK(hipMemcpy(host_out, u->d_out, *out_bytes, hipMemcpyDeviceToHost));
     return BZ2MI_OK;
 }
 

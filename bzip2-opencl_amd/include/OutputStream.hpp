@@ -2,19 +2,30 @@
 // (Stan1slav337/Bzip2-OpenCL include/OutputStream.hpp:35-241), backed by the
 // MI355X device compressor through the C ABI in include/bz2mi.h.
 //
-// Differences in mechanism, not in output:
-//   * blocks are handed to the device in batches of many blocks instead of
-//     `p` at a time (the reference's closeBlocks, :190-240).  The Huffman seed
-//     carry-over still follows block index mod p (its never-cleared per-slot
-//     frequency array), so the bytes are identical for every batch size;
-//   * packed bits instead of bool-per-bit buffers, stitched on the device.
+// Mechanism (the output bytes are the reference's):
+//   * write() only appends raw bytes to a pinned host buffer; the RLE1 front
+//     end, block split and CRCs (the reference's BlockCompressor::write per
+//     byte, OutputStream.hpp:131-142/179-188) run on the device.  The stream is
+//     handed over in units of kUnitBytes (bz2mi_unit_*): a unit's buffer holds
+//     its bytes plus the next bz2mi_unit_halo() bytes, and its block chain
+//     starts where the previous unit's ended.
+//   * two pinned buffers alternate: while the host fills one, the device
+//     compresses the unit copied from the other (RLE1, CRC, BWT, MTF run
+//     asynchronously after the chain); the Huffman / assembly of a unit and
+//     the write of its bytes happen when the next unit is handed over.
+//   * framing on the host as in the reference: "BZh<level>" (:126-128), the
+//     stream CRC chained per block (:202), end-of-stream marker and padding
+//     (:163-176); units are laid out at bit offsets (no byte alignment, the
+//     reference's leftover-bit carry, BitOutputStream.hpp:30-99).
 // Errors: std::invalid_argument for a bad level / parallel count (:73-81),
 // std::runtime_error for writes after close and for device failures (the
 // reference's OpenCL wrapper exits the process instead).
 #ifndef OUTPUT_STREAM_HPP
 #define OUTPUT_STREAM_HPP
 
+#include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <ostream>
 #include <stdexcept>
 #include <string>
@@ -28,7 +39,7 @@ class OutputStream
 {
 public:
     OutputStream(std::ostream &out, int blockSizeMultiplier, int parallelBlockCnt)
-        : out_(out), blockSize_(BLOCKSIZE_DEFAULT * blockSizeMultiplier)
+        : out_(out), level_(blockSizeMultiplier), p_(parallelBlockCnt)
     {
         if (blockSizeMultiplier < 1 || blockSizeMultiplier > 9)
             throw std::invalid_argument("Invalid block size");
@@ -37,25 +48,31 @@ public:
         int device = 0;
         if (const char *d = std::getenv("BZ2MI_DEVICE"))
             device = std::atoi(d);
+        unitBytes_ = kUnitBytes;
+        if (const char *u = std::getenv("BZ2MI_UNIT_BYTES"))  // tests: many small units
+            unitBytes_ = static_cast<size_t>(std::atoll(u));
         ctx_ = bz2mi_create(blockSizeMultiplier, parallelBlockCnt, BLOCKSIZE_DEFAULT, device);
         if (!ctx_)
             throw std::runtime_error(std::string("bz2mi: ") + bz2mi_last_error());
-        stride_ = static_cast<size_t>(blockSize_) + 16;
-        batch_ = kBatchBlocks;
-        blocks_.resize(batch_ * stride_);
-        present_.resize(static_cast<size_t>(batch_) * ALPHABET_SIZE);
-        lens_.resize(batch_);
-        crcs_.resize(batch_);
-        for (int i = 0; i < batch_; ++i)
-            compressors_.emplace_back(blocks_.data() + i * stride_,
-                                      reinterpret_cast<bool *>(present_.data()) + i * ALPHABET_SIZE, blockSize_);
-        staging_.resize(bz2mi_compress_bound(static_cast<size_t>(batch_) * blockSize_, blockSizeMultiplier,
-                                             BLOCKSIZE_DEFAULT));
+        halo_ = bz2mi_unit_halo(blockSizeMultiplier, BLOCKSIZE_DEFAULT);
+        cap_ = unitBytes_ + halo_;
+        for (int i = 0; i < 2; ++i)
+        {
+            buf_[i] = static_cast<unsigned char *>(bz2mi_host_alloc(cap_));
+            unit_[i] = bz2mi_unit_create(ctx_);
+            if (!buf_[i] || !unit_[i])
+            {
+                release();
+                throw std::runtime_error(std::string("bz2mi: ") + bz2mi_last_error());
+            }
+        }
+        sums_.assign(static_cast<size_t>(p_) * 258, 0u);
+        carried_.assign(static_cast<size_t>(p_) * 258, 0u);
     }
 
     ~OutputStream()
     {
-        bz2mi_destroy(ctx_);
+        release();
     }
 
     OutputStream(const OutputStream &) = delete;
@@ -65,11 +82,9 @@ public:
     {
         if (finished_)
             throw std::runtime_error("Write beyond end of stream");
-        if (!compressors_[current_].write(value & 0xff))
-        {
-            nextCompressor();
-            compressors_[current_].write(value & 0xff);
-        }
+        buf_[cur_][fill_++] = static_cast<unsigned char>(value);
+        if (fill_ == cap_)
+            handOver();
     }
 
     void write(const std::vector<char> &data, int offset, int length)
@@ -78,11 +93,13 @@ public:
             throw std::runtime_error("Write beyond end of stream");
         while (length > 0)
         {
-            const int taken = compressors_[current_].write(data, offset, length);
-            if (taken < length)
-                nextCompressor();
-            offset += taken;
-            length -= taken;
+            const size_t take = std::min(static_cast<size_t>(length), cap_ - fill_);
+            std::memcpy(buf_[cur_] + fill_, data.data() + offset, take);
+            fill_ += take;
+            offset += static_cast<int>(take);
+            length -= static_cast<int>(take);
+            if (fill_ == cap_)
+                handOver();
         }
     }
 
@@ -91,44 +108,45 @@ public:
         if (finished_)
             return;
         finished_ = true;
-        flushBlocks(current_ + (compressors_[current_].isEmpty() ? 0 : 1));
-        size_t n = 0;
-        check(bz2mi_finish(ctx_, staging_.data(), staging_.size(), &n));
-        out_.write(reinterpret_cast<const char *>(staging_.data()), static_cast<std::streamsize>(n));
+        finishPending();
+        if (fill_ > 0)
+        {
+            // the last unit: no halo, its blocks run to the end of the stream
+            startUnit(fill_, 0, BZ2MI_UNIT_ENDS_STREAM);
+            finishPending();
+        }
+        if (!headerDone_)  // empty stream: header and trailer only
+        {
+            putBits(0x425a68u, 24);
+            putBits(static_cast<uint32_t>('0' + level_), 8);
+            headerDone_ = true;
+        }
+        // end-of-stream marker, stream CRC, zero padding (OutputStream.hpp:163-176)
+        putBits(0x177245u, 24);
+        putBits(0x385090u, 24);
+        putBits(streamCRC_, 32);
+        if (nbits_ & 7)
+            flushByte();
         out_.flush();
     }
 
 private:
-    static constexpr int kBatchBlocks = 1024;  // blocks per device call
+    static constexpr size_t kUnitBytes = 64ull << 20;  // bytes per unit handed to the device
 
-    void nextCompressor()
+    void release()
     {
-        if (++current_ == batch_)
+        for (int i = 0; i < 2; ++i)
         {
-            flushBlocks(batch_);
-            current_ = 0;
+            if (unit_[i])
+                bz2mi_unit_destroy(unit_[i]);
+            if (buf_[i])
+                bz2mi_host_free(buf_[i]);
+            unit_[i] = nullptr;
+            buf_[i] = nullptr;
         }
-    }
-
-    // close `count` filled blocks and hand them to the device
-    void flushBlocks(int count)
-    {
-        for (int i = 0; i < count; ++i)
-        {
-            BlockCompressor &bc = compressors_[i];
-            bc.finishRLE();
-            lens_[i] = static_cast<uint32_t>(bc.getBlockLength());
-            crcs_[i] = static_cast<uint32_t>(bc.getCRC());
-        }
-        if (count > 0)
-        {
-            size_t n = 0;
-            check(bz2mi_compress_rle1(ctx_, blocks_.data(), stride_, lens_.data(), crcs_.data(),
-                                      static_cast<uint32_t>(count), staging_.data(), staging_.size(), &n));
-            out_.write(reinterpret_cast<const char *>(staging_.data()), static_cast<std::streamsize>(n));
-        }
-        for (int i = 0; i < count; ++i)
-            compressors_[i].reset();
+        if (ctx_)
+            bz2mi_destroy(ctx_);
+        ctx_ = nullptr;
     }
 
     static void check(int rc)
@@ -137,18 +155,107 @@ private:
             throw std::runtime_error(std::string("bz2mi: ") + bz2mi_last_error());
     }
 
+    // buffer full: unit [0, unitBytes_) with the halo [unitBytes_, cap_) goes to
+    // the device; the halo bytes start the next buffer
+    void handOver()
+    {
+        finishPending();
+        startUnit(unitBytes_, halo_, 0);
+        const int nxt = cur_ ^ 1;
+        std::memcpy(buf_[nxt], buf_[cur_] + unitBytes_, halo_);
+        cur_ = nxt;
+        fill_ = halo_;
+    }
+
+    void startUnit(size_t own, size_t halo, int flags)
+    {
+        bz2mi_unit *u = unit_[cur_];
+        check(bz2mi_unit_begin_host(u, buf_[cur_], own, halo, flags));
+        uint64_t exit = 0, nb = 0;
+        check(bz2mi_unit_chain(u, entry_, blocks_, &exit, &nb));
+        entry_ = exit;
+        blocks_ += nb;
+        if (nb)
+        {
+            pending_ = u;
+            pendingBlocks_ = nb;
+        }
+    }
+
+    // Huffman coding and assembly of the unit handed over last, then its bytes
+    void finishPending()
+    {
+        if (!pending_)
+            return;
+        bz2mi_unit *u = pending_;
+        pending_ = nullptr;
+        check(bz2mi_unit_sums(u, sums_.data()));
+        uint64_t bits = 0;
+        uint32_t share = 0;
+        check(bz2mi_unit_encode(u, carried_.data(), &bits, &share));
+        for (size_t i = 0; i < carried_.size(); ++i)
+            carried_[i] += sums_[i];
+        const uint32_t r = static_cast<uint32_t>(pendingBlocks_ & 31u);
+        streamCRC_ = (r ? (streamCRC_ << r) | (streamCRC_ >> (32 - r)) : streamCRC_) ^ share;
+        if (!headerDone_)
+        {
+            putBits(0x425a68u, 24);  // "BZh" + level (OutputStream.hpp:126-128)
+            putBits(static_cast<uint32_t>('0' + level_), 8);
+            headerDone_ = true;
+        }
+        const size_t need = static_cast<size_t>((bits + 7 + 8) / 8) + 16;
+        if (stage_.size() < need)
+            stage_.resize(need + need / 8);
+        size_t n = 0;
+        check(bz2mi_unit_assemble_host(u, nbits_, 0, 0, stage_.data(), stage_.size(), &n));
+        // the first byte shares its top (nbits_ & 7) bits with the pending byte
+        if (n > 0)
+        {
+            stage_[0] |= partial_;
+            const uint64_t end = nbits_ + bits;
+            const size_t whole = static_cast<size_t>(end / 8 - nbits_ / 8);
+            out_.write(reinterpret_cast<const char *>(stage_.data()), static_cast<std::streamsize>(whole));
+            partial_ = (end & 7) ? stage_[whole] : 0;
+            nbits_ = end;
+        }
+    }
+
+    void putBits(uint32_t v, int count)
+    {
+        for (int k = count - 1; k >= 0; --k)
+        {
+            if ((v >> k) & 1u)
+                partial_ |= static_cast<unsigned char>(0x80u >> (nbits_ & 7));
+            ++nbits_;
+            if ((nbits_ & 7) == 0)
+                flushByte();
+        }
+    }
+
+    void flushByte()
+    {
+        out_.put(static_cast<char>(partial_));
+        partial_ = 0;
+        nbits_ = (nbits_ + 7) & ~7ull;
+    }
+
     std::ostream &out_;
-    int blockSize_;
+    int level_;
+    int p_;
     bz2mi_ctx *ctx_ = nullptr;
-    bool finished_ = false;
-    int current_ = 0;
-    int batch_ = 0;
-    size_t stride_ = 0;
-    std::vector<unsigned char> blocks_;
-    std::vector<unsigned char> present_;
-    std::vector<uint32_t> lens_, crcs_;
-    std::vector<BlockCompressor> compressors_;
-    std::vector<uint8_t> staging_;
+    bz2mi_unit *unit_[2] = {nullptr, nullptr};
+    unsigned char *buf_[2] = {nullptr, nullptr};
+    size_t unitBytes_ = 0, halo_ = 0, cap_ = 0, fill_ = 0;
+    int cur_ = 0;
+    bool finished_ = false, headerDone_ = false;
+    uint64_t entry_ = 0, blocks_ = 0;
+    bz2mi_unit *pending_ = nullptr;
+    uint64_t pendingBlocks_ = 0;
+    std::vector<uint32_t> sums_, carried_;
+    uint32_t streamCRC_ = 0;
+    uint64_t nbits_ = 0;     // stream bits so far
+    unsigned char partial_ = 0;  // the byte holding bits [nbits_ & ~7, nbits_)
+    std::vector<uint8_t> stage_;
 };
 
 #endif

@@ -174,6 +174,15 @@ int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, ui
 /* d_out: device memory, 4-byte aligned, >= (bits + 7 + 32 + 80) / 8 + 4 bytes */
 int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags, void* d_out, size_t cap,
                         size_t* out_bytes);
+/* Host-memory forms for C++ hosts without a device allocator (the mirror
+ * OutputStream): begin_host copies the bytes into a unit-owned device buffer
+ * (asynchronous when `host` is pinned; it must stay unchanged until
+ * bz2mi_unit_chain returns); assemble_host copies the unit's bytes back. */
+void* bz2mi_host_alloc(size_t bytes); /* pinned host memory, NULL on failure */
+void bz2mi_host_free(void* p);
+int bz2mi_unit_begin_host(bz2mi_unit* u, const void* host, size_t n_own, size_t n_halo, int flags);
+int bz2mi_unit_assemble_host(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags, void* host_out,
+                             size_t cap, size_t* out_bytes);
 /* milliseconds of the unit's stages (HIP events): front scan, chain (host wall),
  * RLE1 + CRC + BWT, MTF, Huffman, assembly */
 int bz2mi_unit_timings(bz2mi_unit* u, float* ms6);

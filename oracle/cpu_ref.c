@@ -414,6 +414,12 @@ static int table_count(int mtfLength) { /* kernel.cpp:2808-2818 */
 static inline int32_t wadd(int32_t a, uint32_t b) { return (int32_t)((uint32_t)a + b); }
 static inline int32_t wsub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
 
+/* H3 as the reference behaves on an MI355X (tests/test_refgpu.py): the
+ * uninitialised tableFrequencies (kernel.cpp:2902) starts at zero in a lane's
+ * first block but is not cleared between the four optimisation passes. */
+static int h3_accumulate = 0;
+void cpuref_set_h3_accumulate(int on) { h3_accumulate = on; }
+
 long long cpuref_block_payload(int origPtr, const uint8_t* present, const uint16_t* mtf,
                                int mtfLength, int alpha, const uint32_t* seed, uint8_t* out,
                                uint64_t cap_bits, uint8_t* sel_out, uint8_t* len_out) {
@@ -458,9 +464,10 @@ long long cpuref_block_payload(int origPtr, const uint8_t* present, const uint16
         }
     }
     /* 4x optimiseSelectorsAndHuffmanTables, kernel.cpp:2895-2951 */
+    static __thread int tf[6][258];
+    memset(tf, 0, sizeof(tf));
     for (int it = 3; it >= 0; it--) {
-        static __thread int tf[6][258];
-        memset(tf, 0, sizeof(tf)); /* H3: zero-initialised */
+        if (!h3_accumulate) memset(tf, 0, sizeof(tf)); /* H3: zero-initialised per pass (O_ref) */
         int si = 0;
         for (int gs = 0; gs < mtfLength;) {
             int ge = (gs + 50 < mtfLength ? gs + 50 : mtfLength) - 1;

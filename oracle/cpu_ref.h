@@ -54,6 +54,11 @@ long long cpuref_block_payload(int origPtr, const uint8_t* present, const uint16
                                int mtfLength, int alpha, const uint32_t* seed, uint8_t* out,
                                uint64_t cap_bits, uint8_t* selectors, uint8_t* lengths);
 
+/* H3 model of the reference run on an MI355X (OpenCL): tableFrequencies not
+ * cleared between the four optimisation passes of a block (default off = O_ref,
+ * zero-initialised per pass).  Process-wide; set before compressing. */
+void cpuref_set_h3_accumulate(int on);
+
 /* ---- whole stream (OutputStream.hpp semantics): level 1..9, parallel count
  *      p >= 1, block unit (10000 = reference, 100000 = 900 KB mode).
  *      threads > 1 compresses blocks on a pthread pool.  Returns the output

@@ -126,8 +126,10 @@ def test_device_api_and_context_reuse(bz):
     assert s1 == s2 == bz.compress(data.tobytes(), 9, 10)
 
 
-def test_full_size_random_round_trip(bz):
-    """BASELINE config C2 at full size: 1 GiB random bytes at -9 decode back."""
+def test_full_size_random_round_trip(bz, cpuref):
+    """BASELINE config C2 at full size: the 1 GiB stream at -9, p = 10 is the C
+    restatement's (cpu_ref on the host's cores, pinned to O_ref) byte for
+    byte, and decodes back with libbz2."""
     import torch
     n = 1 << 30
     g = torch.Generator(device="cuda")
@@ -140,7 +142,10 @@ def test_full_size_random_round_trip(bz):
     stream = out[:m].cpu().numpy().tobytes()
     del out
     assert stream[:4] == b"BZh9"
-    assert bz2.decompress(stream) == x.cpu().numpy().tobytes()
+    host = x.cpu().numpy().tobytes()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    assert stream == cpuref.compress(host, 9, 10, threads=threads)
+    assert bz2.decompress(stream) == host
 
 
 OS_HARNESS = r"""
