@@ -100,9 +100,7 @@ int stage_front(bz2mi_ctx* c, Batch& t, const FrontBufs& f, const uint8_t* d_x, 
                 uint64_t cnt, hipStream_t s) {
     using namespace bz2mi;
     hipLaunchKernelGGL(fe_rle1_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, f.d_starts, first,
-                       cnt, t.d_blocks, c->stride, t.d_lens);
-    hipLaunchKernelGGL(fe_crc_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, f.d_starts, first, cnt,
-                       t.d_crc, c->d_crctab);
+                       cnt, t.d_blocks, c->stride, t.d_lens, t.d_crc, c->d_crctab);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("front-rle1");
     return BZ2MI_OK;
@@ -235,7 +233,7 @@ int stage_seed(bz2mi_ctx* c, Batch& t, int nb, uint64_t first_block, uint32_t* s
 int stage_huffman(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     using namespace bz2mi;
     const size_t sel_bytes = ((size_t)(c->S + 1 + 49) / 50 + 15) & ~(size_t)15;
-    hipLaunchKernelGGL(huffman_kernel, dim3(nb), dim3(256), sel_bytes, s, t.d_mtf, c->mtf_stride, t.d_mtflen, t.d_alpha,
+    hipLaunchKernelGGL(huffman_kernel, dim3(nb), dim3(huffman_threads()), sel_bytes, s, t.d_mtf, c->mtf_stride, t.d_mtflen, t.d_alpha,
                        t.d_seed, t.d_present, t.d_orig, nb, t.d_payload, c->payload_words, t.d_pbits);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("huffman");
@@ -653,8 +651,10 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
         return nullptr;
     }
     (void)hipMemset(c->d_state, 0, sizeof(uint32_t) * c->p * bz2mi::kMaxAlpha);
-    if (dalloc(&c->d_crctab, 256) ||
-        hipMemcpy(c->d_crctab, bz2mi::kCrc.t.data(), 256 * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    std::vector<uint32_t> crctabs(bz2mi::kCrcTabWords);
+    bz2mi::crc_device_tables(crctabs.data());
+    if (dalloc(&c->d_crctab, crctabs.size()) ||
+        hipMemcpy(c->d_crctab, crctabs.data(), crctabs.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
         bz2mi_destroy(c);
         return nullptr;
     }

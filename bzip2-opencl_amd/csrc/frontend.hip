@@ -22,6 +22,7 @@
 // that re-phases the run's 255-byte pieces from the block start.
 #include "common.hpp"
 #include "kernels.hpp"
+#include "rle1.hpp"
 
 namespace bz2mi {
 
@@ -249,8 +250,11 @@ __global__ __launch_bounds__(256) void fe_cost_kernel(const uint8_t* __restrict_
     }
     uint64_t before = __shfl_up(xs, 1);
     if (lane == 0) before = 0;
-    // run start in effect before this lane's first byte
-    uint64_t cur = before ? before - 1 : (c == 0 ? 0 : rsb[c]);
+    // run start in effect before this lane's first byte; ph = (i - cur) % 255,
+    // the position of byte i in its run's current 255-byte piece, kept
+    // incrementally (one 64-bit modulo per lane, not per byte)
+    const uint64_t cur = before ? before - 1 : (c == 0 ? 0 : rsb[c]);
+    uint32_t ph = (uint32_t)((at - cur) % 255u);
     uint32_t sum = 0;
     uint32_t packed[16];
 #pragma unroll
@@ -258,21 +262,18 @@ __global__ __launch_bounds__(256) void fe_cost_kernel(const uint8_t* __restrict_
 #pragma unroll
     for (int q = 0; q < 64; ++q) {
         const uint32_t pos = (uint32_t)lane * 64 + q;
-        const uint64_t i = c0 + pos;
         uint32_t cst = 0;
         if (pos < len) {
             const uint32_t prev = q ? v[q - 1] : prev_last;
             const bool rs = (pos == 0) ? chunk_rs : (v[q] != prev);
             if (rs) {
-                if (i > 0) {
-                    const uint32_t part = (uint32_t)((i - cur) % 255u);
-                    cst = piece_cost(part);
-                }
-                cur = i;
-            } else if ((i - cur) % 255u == 254u) {
+                if (c0 + pos > 0) cst = piece_cost(ph);
+                ph = 0;
+            } else if (ph == 254u) {
                 cst = 5;
             }
         }
+        ph = ph == 254u ? 0u : ph + 1u;
         sum += cst;
         packed[q >> 2] |= cst << ((q & 3) * 8);
     }
@@ -886,47 +887,59 @@ __global__ __launch_bounds__(256) void fe_resolve_kernel(const uint8_t* __restri
     }
 }
 
-namespace {
 
-// CRC register map "process L zero bytes" as 32 columns; apply to v.
-__device__ __forceinline__ uint32_t mat_apply(const uint32_t* col, uint32_t v) {
-    uint32_t r = 0;
-#pragma unroll 8
-    for (int b = 0; b < 32; ++b)
-        if (v >> b & 1u) r ^= col[b];
-    return r;
-}
-
-}  // namespace
-
-// ---- K8: RLE1 emission, one workgroup per block, tiles of 4096 input bytes:
-// the tile (and the byte before it) is staged in LDS with 16-byte loads,
-// each thread emits its 16 bytes into an LDS copy of the tile's output, which
-// is then written out contiguously.  A count byte that belongs to a piece
-// begun in an earlier tile is written straight to the block.
+// ---- K8: RLE1 emission and block CRC, one workgroup per block, tiles of
+// 4096 input bytes: the tile (and the bytes before it the CRC needs) is staged
+// in LDS with 16-byte loads, each thread emits its 16 bytes into an LDS copy
+// of the tile's output, which is then written out contiguously.  A count byte
+// that belongs to a piece begun in an earlier tile is written straight to the
+// block.
+// Block CRC (CRC32.hpp:75-86 over the input bytes [p0, p1)): the block is
+// viewed front-padded with zero bytes to whole 4096-byte tiles (leading zeros
+// leave a raw CRC register at 0), so thread t always owns bytes [16t, 16t+16)
+// of every padded tile: it folds their raw CRC into its accumulator
+// acc = A_4096(acc) ^ crc16 (Horner over the tiles); the block's raw CRC is the
+// ordered combination of the 256 accumulators (a tree with the maps
+// A_{16*2^l}), and crc = ~(A_len(0xffffffff) ^ raw).
 constexpr int kTile = 4096;
 constexpr int kTileOut = kTile + kTile / 4 + 16;
+
+__device__ __forceinline__ uint32_t crc_map(const uint32_t* __restrict__ T, uint32_t x) {
+    return T[x & 255u] ^ T[256 + ((x >> 8) & 255u)] ^ T[512 + ((x >> 16) & 255u)] ^ T[768 + (x >> 24)];
+}
 
 __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict__ x, uint64_t n,
                                                       const uint64_t* __restrict__ starts, uint64_t first, uint64_t count,
                                                       uint8_t* __restrict__ blocks, size_t stride,
-                                                      uint32_t* __restrict__ lens) {
-    __shared__ uint4 tin4[kTile / 16 + 4];
+                                                      uint32_t* __restrict__ lens, uint32_t* __restrict__ crcs,
+                                                      const uint32_t* __restrict__ crc_tabs) {
+    __shared__ uint4 tin4[2 * kTile / 16 + 4];
     __shared__ uint8_t tout[kTileOut];
     __shared__ uint32_t tmp[8];
     __shared__ uint32_t lastv[256];
+    __shared__ uint32_t tslice[1024], t4096[1024];
     const uint64_t lb = blockIdx.x;  // batch-local block
     if (lb >= count) return;
     const uint64_t b = first + lb;
     const int t = threadIdx.x;
     const uint64_t p0 = starts[b], p1 = starts[b + 1];
     uint8_t* out = blocks + lb * stride;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tslice[t + 256 * k] = crc_tabs[t + 256 * k];
+        t4096[t + 256 * k] = crc_tabs[kCrcShiftBase + 1024 * 12 + t + 256 * k];
+    }
+    const uint64_t pad = (kTile - (p1 - p0) % kTile) % kTile;
+    uint32_t acc = 0;
     const uint8_t* tin = reinterpret_cast<const uint8_t*>(tin4);
     uint32_t o_carry = 0;
     uint64_t rs_carry = p0;  // run start in effect before the tile
     for (uint64_t base = p0; base < p1; base += kTile) {
-        // stage [abase, abase + 16*nvec) covering base-1 .. base+kTile
-        const uint64_t abase = base ? ((base - 1) & ~15ull) : 0;
+        // stage [abase, abase + 16*nvec) covering base-1 .. base+kTile and the
+        // CRC bytes from base - pad on
+        const uint64_t lo = base == p0 ? p0 : base - pad;
+        const uint64_t lo1 = base < lo + 1 ? base : lo + 1;
+        const uint64_t abase = lo1 ? ((lo1 - 1) & ~15ull) : 0;
         const uint64_t aend = min(n, base + kTile + 1);
         const int nvec = (int)((aend - abase + 15) >> 4);
         for (int v = t; v < nvec; v += 256) {
@@ -942,6 +955,24 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         }
         __syncthreads();
         const uint32_t off0 = (uint32_t)(base - abase);
+        {  // CRC of padded-tile bytes [16t, 16t+16): real positions base - pad + 16t + k
+            const int64_t r0 = (int64_t)base - (int64_t)pad + 16 * t;
+            uint32_t r = 0;
+#pragma unroll
+            for (int w4 = 0; w4 < 4; ++w4) {
+                uint32_t wd = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int64_t rp = r0 + 4 * w4 + k;
+                    const uint32_t by = rp >= (int64_t)p0 ? (uint32_t)tin[(uint64_t)rp - abase] : 0u;
+                    wd = (wd << 8) | by;
+                }
+                const uint32_t xw = r ^ wd;
+                r = tslice[768 + (xw >> 24)] ^ tslice[512 + ((xw >> 16) & 255u)] ^ tslice[256 + ((xw >> 8) & 255u)] ^
+                    tslice[xw & 255u];
+            }
+            acc = (base == p0) ? r : crc_map(t4096, acc) ^ r;
+        }
         const uint64_t a = base + (uint64_t)t * 16;
         uint8_t v[16];
 #pragma unroll
@@ -963,31 +994,39 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         lastv[t] = mx;
         __syncthreads();
         const uint32_t ex = t ? lastv[t - 1] : 0u;  // exclusive max over earlier threads
-        uint64_t cur = ex ? p0 + ex - 1 : rs_carry;
+        // u = (i - run start) % 255 of byte i, kept incrementally from the
+        // thread's first byte (one 64-bit modulo per thread and tile)
+        const uint64_t cur = ex ? p0 + ex - 1 : rs_carry;
+        const uint32_t u0 = a < p1 ? (uint32_t)((a - cur) % 255u) : 0u;
         // emission counts
         uint32_t e = 0;
+        uint32_t u = u0;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const uint64_t i = a + q;
             if (i < p1) {
                 const uint32_t pv = q ? v[q - 1] : prev;
-                if (i == p0 || v[q] != pv) cur = i;
-                const uint32_t u = (uint32_t)((i - cur) % 255u);
+                if (i == p0 || v[q] != pv) u = 0;
                 e += u < 3 ? 1u : (u == 3 ? 2u : 0u);
             }
+            u = u == 254u ? 0u : u + 1u;
         }
         uint32_t etot;
         const uint32_t eoff = wg_excl_sum<256>(e, tmp, &etot);
         // emit into the LDS copy (o: block-relative output position)
         uint32_t o = o_carry + eoff;
-        cur = ex ? p0 + ex - 1 : rs_carry;
+        uint32_t un = u0;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const uint64_t i = a + q;
+            uint32_t u = un;
+            un = u == 254u ? 0u : u + 1u;
             if (i < p1) {
                 const uint32_t pv = q ? v[q - 1] : prev;
-                if (i == p0 || v[q] != pv) cur = i;
-                const uint32_t u = (uint32_t)((i - cur) % 255u);
+                if (i == p0 || v[q] != pv) {
+                    u = 0;
+                    un = 1;
+                }
                 const uint32_t nx = q < 15 ? v[q + 1] : nextb;
                 const bool last = (i + 1 == p1) || nx != v[q] || u == 254;
                 if (u < 3) {
@@ -1010,132 +1049,29 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         __syncthreads();
     }
     if (t == 0) lens[lb] = o_carry;
-}
-
-// ---- K9: block CRC over the input bytes [p0, p1), one workgroup per block.
-// Thread t takes L contiguous bytes (L a multiple of 4, the range padded at
-// the front with virtual zero bytes: crc0 of leading zeros is 0), reads them
-// as aligned dwords and runs a slicing-by-4 CRC; the 256 partial CRCs are then
-// combined by an ordered tree with the maps A_{L*2^l} ("L zero bytes").
-__global__ __launch_bounds__(256) void fe_crc_kernel(const uint8_t* __restrict__ x, uint64_t n,
-                                                     const uint64_t* __restrict__ starts, uint64_t first, uint64_t count,
-                                                     uint32_t* __restrict__ crcs, const uint32_t* __restrict__ crc_table) {
-    __shared__ uint32_t tab[4][256];
-    __shared__ uint32_t colA[8][32];   // A_{L * 2^l}
-    __shared__ uint32_t colT[32];      // A_len
-    __shared__ uint32_t colW[32];
-    __shared__ uint32_t part[256];
-    const uint64_t lb = blockIdx.x;
-    if (lb >= count) return;
-    const uint64_t b = first + lb;
-    const int t = threadIdx.x;
-    tab[0][t] = crc_table[t];
-    __syncthreads();
-    for (int k = 1; k < 4; ++k) {
-        const uint32_t pv = tab[k - 1][t];
-        tab[k][t] = (pv << 8) ^ tab[0][pv >> 24];
-        __syncthreads();
-    }
-    const uint64_t p0 = starts[b], p1 = starts[b + 1];
-    const uint64_t len_in = p1 - p0;
-    const uint64_t L = (((len_in + 255) / 256) + 3) & ~3ull;
-    const int64_t s0 = (int64_t)p1 - 256 * (int64_t)L;  // first (virtual) byte
-    uint32_t r = 0;
-    {
-        const int64_t start = s0 + (int64_t)t * (int64_t)L;
-        const int64_t astart = start >= 0 ? (start & ~3ll) : -((-start + 3) & ~3ll);
-        const uint32_t sh = (uint32_t)(start - astart);  // 0..3
-        auto dword_at = [&](int64_t ad) -> uint32_t {  // little-endian dword of bytes [ad, ad+4), zero outside [p0, p1)
-            if (ad >= (int64_t)p0 && ad + 4 <= (int64_t)p1) return *reinterpret_cast<const uint32_t*>(x + ad);
-            uint32_t w = 0;
-            for (int q = 0; q < 4; ++q) {
-                const int64_t j = ad + q;
-                if (j >= (int64_t)p0 && j < (int64_t)p1) w |= (uint32_t)x[j] << (8 * q);
-            }
-            return w;
-        };
-        uint32_t lo = dword_at(astart);
-        const int nw = (int)(L >> 2);
-        for (int kk = 0; kk < nw; kk += 8) {
-            uint32_t hi[8];
+    // ordered combination of the accumulators: level l joins neighbours of
+    // 16 * 2^l padded bytes each (in-wave levels by shuffles, then LDS)
+    uint32_t v = acc;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) hi[q] = kk + q < nw ? dword_at(astart + 4 * (kk + q + 1)) : 0u;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if (kk + q < nw) {
-                    const uint32_t wle = sh ? __builtin_amdgcn_alignbyte(hi[q], lo, sh) : lo;
-                    const uint32_t xw = r ^ __builtin_bswap32(wle);
-                    r = tab[3][xw >> 24] ^ tab[2][(xw >> 16) & 255u] ^ tab[1][(xw >> 8) & 255u] ^ tab[0][xw & 255u];
-                    lo = hi[q];
-                }
-            }
-        }
+    for (int l = 0; l < 6; ++l) {
+        const uint32_t right = (uint32_t)__shfl_down((int)v, 1 << l);
+        if ((t & ((2 << l) - 1)) == 0) v = crc_map(crc_tabs + kCrcShiftBase + 1024 * (l + 4), v) ^ right;
     }
-    part[t] = r;
-    const uint32_t* ctab = tab[0];
-    // A_1 columns, then A_L, A_{2L}, ... by squaring/multiplying (thread k owns column k)
+    if ((t & 63) == 0) lastv[t >> 6] = v;
     __syncthreads();
-    if (t < 32) {
-        const uint32_t e1 = 1u << t;
-        colW[t] = (e1 << 8) ^ ctab[e1 >> 24];  // A_1
+    if (t == 0) {
+        const uint32_t* A1024 = crc_tabs + kCrcShiftBase + 1024 * 10;
+        const uint32_t* A2048 = crc_tabs + kCrcShiftBase + 1024 * 11;
+        const uint32_t left = crc_map(A1024, lastv[0]) ^ lastv[1];
+        const uint32_t right = crc_map(A1024, lastv[2]) ^ lastv[3];
+        const uint32_t raw = crc_map(A2048, left) ^ right;
+        // the initial register 0xffffffff processed over the block's length
+        uint32_t init = 0xffffffffu;
+        const uint64_t len = p1 - p0;
+        for (int k = 0; k < 40 && (len >> k); ++k)
+            if ((len >> k) & 1u) init = crc_map(crc_tabs + kCrcShiftBase + 1024 * k, init);
+        crcs[lb] = ~(init ^ raw);
     }
-    __syncthreads();
-    // A_L via binary powering: acc = I
-    if (t < 32) colA[0][t] = 1u << t;
-    __syncthreads();
-    for (uint64_t e2 = L; e2; e2 >>= 1) {
-        if (e2 & 1) {
-            uint32_t c = 0;
-            if (t < 32) c = mat_apply(colW, colA[0][t]);
-            __syncthreads();
-            if (t < 32) colA[0][t] = c;
-            __syncthreads();
-        }
-        uint32_t c2 = 0;
-        if (t < 32) c2 = mat_apply(colW, colW[t]);
-        __syncthreads();
-        if (t < 32) colW[t] = c2;
-        __syncthreads();
-    }
-    for (int l = 1; l < 8; ++l) {
-        uint32_t c = 0;
-        if (t < 32) c = mat_apply(colA[l - 1], colA[l - 1][t]);
-        __syncthreads();
-        if (t < 32) colA[l][t] = c;
-        __syncthreads();
-    }
-    // ordered tree: level l combines left (2^l*L bytes) and right: left' = A_{2^l L}(left) ^ right
-    for (int l = 0; l < 8; ++l) {
-        const int stride2 = 1 << (l + 1);
-        uint32_t v = 0;
-        const bool act = (t % stride2) == 0;
-        if (act) v = mat_apply(colA[l], part[t]) ^ part[t + (stride2 >> 1)];
-        __syncthreads();
-        if (act) part[t] = v;
-        __syncthreads();
-    }
-    // A_len for the initial register 0xffffffff
-    if (t < 32) {
-        colT[t] = 1u << t;
-        const uint32_t e1 = 1u << t;
-        colW[t] = (e1 << 8) ^ ctab[e1 >> 24];
-    }
-    __syncthreads();
-    for (uint64_t e2 = len_in; e2; e2 >>= 1) {
-        if (e2 & 1) {
-            uint32_t c = 0;
-            if (t < 32) c = mat_apply(colW, colT[t]);
-            __syncthreads();
-            if (t < 32) colT[t] = c;
-            __syncthreads();
-        }
-        uint32_t c2 = 0;
-        if (t < 32) c2 = mat_apply(colW, colW[t]);
-        __syncthreads();
-        if (t < 32) colW[t] = c2;
-        __syncthreads();
-    }
-    if (t == 0) crcs[lb] = ~(mat_apply(colT, 0xffffffffu) ^ part[0]);
 }
 
 }  // namespace bz2mi

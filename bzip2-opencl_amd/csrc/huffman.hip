@@ -33,7 +33,12 @@ BZ2MI_PHASE_TABLE(g_huf_phase)
 
 namespace {
 
-constexpr int NT = 256;
+// BZ2MI_HUF_NT: threads per workgroup (a multiple of 64); with 6 or more
+// waves every table's code lengths are built on a wave of its own
+#ifndef BZ2MI_HUF_NT
+#define BZ2MI_HUF_NT 256
+#endif
+constexpr int NT = BZ2MI_HUF_NT;
 constexpr int NW = NT / 64;
 constexpr int kTileSyms = 8 * NT;                    // symbols per data tile
 constexpr int kWinWords = kTileSyms * kMaxCodeLen / 32 + 2;
@@ -231,8 +236,8 @@ __device__ __forceinline__ int table_count(int m) {
     return m >= 2400 ? 6 : m >= 1200 ? 5 : m >= 600 ? 4 : m >= 200 ? 3 : 2;
 }
 
-// table q is handled by wave q % 4
-__device__ __forceinline__ bool my_table(int q) { return (q & (NW - 1)) == wave_id(); }
+// table q is handled by wave q % NW
+__device__ __forceinline__ bool my_table(int q) { return q % NW == wave_id(); }
 
 // ascending register bitonic sort of 64*E keys over one wave, striped
 // (element e of lane l is item e*64 + l)
@@ -302,7 +307,7 @@ __device__ void build_table(HufShared& sh, int q, int alpha) {
         if (e * 64 + lane < alpha) sh.lens[q][key[e] & 511u] = (uint8_t)v[e];
 }
 
-// code lengths of every table, table q on wave q%4
+// code lengths of every table, table q on wave q%NW
 __device__ void build_lengths(HufShared& sh, int T, int alpha) {
     for (int q = 0; q < T; ++q)
         if (my_table(q)) build_table(sh, q, alpha);
@@ -388,7 +393,9 @@ int huffman_phases(unsigned long long* out) {
 #ifndef BZ2MI_HUF_WGS
 #define BZ2MI_HUF_WGS 6
 #endif
-__global__ __launch_bounds__(256, BZ2MI_HUF_WGS) void huffman_kernel(
+int huffman_threads() { return NT; }
+
+__global__ __launch_bounds__(NT, BZ2MI_HUF_WGS) void huffman_kernel(
     const uint16_t* __restrict__ mtf, size_t mtf_stride, const uint32_t* __restrict__ mtf_len,
     const uint32_t* __restrict__ alpha_in, const uint32_t* __restrict__ seed,
     const uint32_t* __restrict__ present, const uint32_t* __restrict__ orig, int nblocks,

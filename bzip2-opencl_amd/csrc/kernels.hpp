@@ -86,6 +86,7 @@ int bwt_phases(unsigned long long* out);
 int mtf_phases(unsigned long long* out);
 int fe_phases(unsigned long long* out);
 int run_selftest(uint32_t* host_bad, int n);  // cross-lane primitive checks
+int huffman_threads();  // workgroup size of huffman_kernel
 __global__ void huffman_kernel(const uint16_t* mtf, size_t mtf_stride, const uint32_t* mtf_len,
                                const uint32_t* alpha_in, const uint32_t* seed, const uint32_t* present,
                                const uint32_t* orig, int nblocks, uint32_t* payload, size_t payload_words,
@@ -136,9 +137,9 @@ __global__ void fe_chain_kernel(const uint8_t* x, const uint8_t* cost, const uin
 __global__ void fe_resolve_kernel(const uint8_t* x, const uint8_t* cost, const uint64_t* fc, const uint4* summ,
                                   uint64_t n, uint64_t nc, uint64_t n_own, uint64_t entry, const uint64_t* bnd,
                                   uint64_t* nb_io, uint64_t* starts);
+// RLE1 emission + block CRCs (crc_tabs: rle1.hpp crc_device_tables)
 __global__ void fe_rle1_kernel(const uint8_t* x, uint64_t n, const uint64_t* starts, uint64_t first, uint64_t count,
-                               uint8_t* blocks, size_t stride, uint32_t* lens);
-__global__ void fe_crc_kernel(const uint8_t* x, uint64_t n, const uint64_t* starts, uint64_t first, uint64_t count,
-                              uint32_t* crcs, const uint32_t* crc_table);
+                               uint8_t* blocks, size_t stride, uint32_t* lens, uint32_t* crcs,
+                               const uint32_t* crc_tabs);
 
 }  // namespace bz2mi

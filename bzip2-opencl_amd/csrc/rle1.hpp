@@ -27,6 +27,43 @@ struct Crc32Table {
 };
 inline constexpr Crc32Table kCrc{};
 
+// Device CRC tables (layout of kCrcTabWords u32): [0, 1024) slicing-by-4
+// tables (T_k[b] = CRC register of byte b followed by k zero bytes), then for
+// k = 0..31 the linear map "process 2^k zero bytes" on a raw CRC register as
+// four byte-sliced tables (1024 words each): A(x) = T0[x&255] ^ T1[x>>8&255] ^
+// T2[x>>16&255] ^ T3[x>>24].  Used to combine CRCs of byte ranges computed in
+// parallel: crc(A|B) = A_{|B|}(crc(A)) ^ crc(B) for raw registers.
+constexpr int kCrcShiftBase = 1024;
+constexpr int kCrcTabWords = 1024 * 33;
+inline void crc_device_tables(uint32_t* out) {
+    for (int b = 0; b < 256; ++b) {
+        uint32_t v = kCrc.t[b];
+        out[b] = v;
+        for (int k = 1; k < 4; ++k) {
+            v = (v << 8) ^ kCrc.t[v >> 24];
+            out[256 * k + b] = v;
+        }
+    }
+    uint32_t col[32], sq[32];
+    for (int i = 0; i < 32; ++i) {  // A_1: one zero byte
+        const uint32_t e = 1u << i;
+        col[i] = (e << 8) ^ kCrc.t[e >> 24];
+    }
+    auto apply = [](const uint32_t* c, uint32_t x) {
+        uint32_t r = 0;
+        for (int i = 0; i < 32; ++i)
+            if (x >> i & 1u) r ^= c[i];
+        return r;
+    };
+    for (int k = 0; k < 32; ++k) {
+        uint32_t* T = out + kCrcShiftBase + 1024 * k;
+        for (int j = 0; j < 4; ++j)
+            for (uint32_t b = 0; b < 256; ++b) T[256 * j + b] = apply(col, b << (8 * j));
+        for (int i = 0; i < 32; ++i) sq[i] = apply(col, col[i]);  // A_{2^(k+1)} = A_{2^k} o A_{2^k}
+        for (int i = 0; i < 32; ++i) col[i] = sq[i];
+    }
+}
+
 inline uint32_t crc_update(uint32_t crc, const uint8_t* p, size_t n) {
     for (size_t i = 0; i < n; ++i) crc = (crc << 8) ^ kCrc.t[((crc >> 24) ^ p[i]) & 0xffu];
     return crc;
