@@ -75,6 +75,7 @@ int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks) {
     if ((r = dalloc(&t.d_bcnt, 1024))) return r;
     if ((r = dalloc(&t.d_ngroups, B))) return r;
     if ((r = dalloc(&t.d_p2list, B))) return r;
+    if ((r = dalloc(&t.d_redo, B))) return r;
     if ((r = dalloc(&t.d_groups, B * bz2mi::bwt_group_stride(c->stride)))) return r;
     if ((r = dalloc(&t.d_mtf, B * c->mtf_stride))) return r;
     if ((r = dalloc(&t.d_mtflen, B))) return r;
@@ -157,9 +158,11 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     const uint32_t smask = blk ? 0xffffffffu : (uint32_t)(kBwtShards - 1);
     if (blk) {
         HIPCHECK(hipMemsetAsync(c->d_scb, 0, nb * sizeof(uint32_t), s));
-        hipLaunchKernelGGL(bwt_block_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
-                           t.d_bwt, t.d_orig, c->d_lq[1], lcount + kBwtShards, lcap, t.d_present, c->d_tq[0], tc[0],
-                           tcap);
+        HIPCHECK(hipMemsetAsync(t.d_redo, 0, nb * sizeof(uint32_t), s));
+        for (int mode = 0; mode < (bwt_safree() ? 2 : 1); ++mode)
+            hipLaunchKernelGGL(bwt_block_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
+                               t.d_sa, t.d_bwt, t.d_orig, c->d_lq[1], lcount + kBwtShards, lcap, t.d_present,
+                               c->d_tq[0], tc[0], tcap, t.d_redo, mode);
     } else {
         hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
                            t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap,

@@ -203,8 +203,13 @@ struct GroupSink {
     uint32_t block;
     uint64_t* tq;        // non-null: tie groups go to this global queue (with their depth)
     uint32_t* tcount;
+    uint32_t* redo;      // non-null (SA-free pass): a group marks the block for the SA path instead
 
     __device__ __forceinline__ void push(Seg g) const {
+        if (redo) {
+            *redo = 1u;
+            return;
+        }
         const uint32_t slot = atomicAdd(counter, 1u);
         if (slot < cap) out[slot] = g;
         if (worklist && slot == 0) worklist[atomicAdd(wcount, 1u)] = block;
@@ -213,6 +218,10 @@ struct GroupSink {
     // rotations share `depth` bytes.  Tie-queue pushes take one atomic per
     // wave (the queue counter is shared by the whole chip).
     __device__ __forceinline__ void push_agg(bool want, Seg g, uint32_t depth) const {
+        if (redo) {
+            if (__ballot(want) && lane_id() == 0) *redo = 1u;
+            return;
+        }
         if (!tq) {
             if (want) push(g);
             return;
@@ -324,7 +333,7 @@ __device__ __forceinline__ void wave_sort_emit(const uint8_t* __restrict__ T, in
         const uint32_t i = MODE == 0 ? lo[e] & 0xffffffu : (uint32_t)(key[e] & ((1u << kIdxBits) - 1u));
         const uint32_t gs = gsl[e] > before ? gsl[e] : before;
         if (valid) {
-            s.sa[seg.start + g] = i;
+            if (MODE != 0 || s.sa) s.sa[seg.start + g] = i;
             if (MODE == 0) {
                 bwt[seg.start + g] = (uint8_t)(lo[e] >> 24);
                 if (i == 0) *orig = seg.start + g;
@@ -801,7 +810,7 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
         }
         const uint32_t fin = seg.start + b0 + lt + eqlt;
         if (mine) {
-            s.sa[fin] = i;
+            if (s.sa) s.sa[fin] = i;
             bwt[fin] = (uint8_t)(ii >> 24);
             if (i == 0) *orig = fin;
         }
@@ -1366,11 +1375,34 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
 constexpr int FT = 1024;
 constexpr int FW = FT / 64;
 
+// SA-free pass (blocks whose first-byte buckets are all <= kSmall): the
+// rotation indices of a run of batches are staged in LDS (kPassIdx at a time)
+// and sorted in place there; each wave keeps only its sub-bucket bases.  It
+// removes the SA round trips (8.6 GB per GiB of random input) but measured
+// slower -- random BWT 12.5 -> 17.6 ms per GiB: a text scan and two barriers
+// per pass of ~32 batches cost more than the global first-byte scatter they
+// replace -- so it is off (BZ2MI_BWT_SAFREE=1 builds it in, bwt_safree()).
+#ifndef BZ2MI_BWT_SAFREE
+#define BZ2MI_BWT_SAFREE 0
+#endif
+constexpr bool kBwtSaFree = BZ2MI_BWT_SAFREE != 0;
+constexpr int kPassIdx = 11264;
+
+struct BucketRef {  // a batch's LDS slice (Bucket3Lds layout by pointer)
+    static constexpr bool kKeys = false;
+    uint32_t* base;
+    uint32_t* idx;
+};
+
 struct BlockLds {
     uint4 text[kBwtLdsText / 16];
     union {
         uint32_t stage[FT * 8];
         Bucket3Lds w[FW];
+        struct {
+            uint32_t base[FW][257];
+            uint32_t idx[kPassIdx];
+        } pass;
     } u;
     BwtShared sh;
     uint32_t th[256], ts[256], tmp[FW];
@@ -1382,11 +1414,14 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
                                                        uint32_t* __restrict__ orig_out, BwtItem* __restrict__ lq,
                                                        uint32_t* __restrict__ lcount, size_t lcap,
                                                        uint32_t* __restrict__ present_out, uint64_t* __restrict__ tl,
-                                                       uint32_t* __restrict__ tcount, size_t tcap) {
+                                                       uint32_t* __restrict__ tcount, size_t tcap,
+                                                       uint32_t* __restrict__ redo, int mode) {
     __shared__ BlockLds L;
     BwtShared& sh = L.sh;
     const int b = blockIdx.x;
     if (b >= nblocks) return;
+    // mode 1: only the blocks the SA-free pass of mode 0 handed back
+    if (mode == 1 && redo[b] == 0u) return;
     const int t = threadIdx.x;
     const int n = (int)uniform(lens[b]);
     const uint8_t* T = blocks + (size_t)b * stride;
@@ -1423,6 +1458,81 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     uint32_t total;
     const uint32_t ex = wg_excl_sum<FT>(c, L.tmp, &total);
     if (t < 256) sh.base[t] = ex;
+    if (kBwtSaFree && mode == 0 && !__syncthreads_or(c > (uint32_t)kSmall)) {
+        // ---- SA-free pass: every bucket is small, so the whole BWT is the
+        // batch sorts.  Runs of batches of up to kPassIdx rotations: their
+        // indices are staged in LDS by a scan of the LDS text, sorted in place
+        // by one wave per batch, and only BWT bytes and origPtr leave the
+        // workgroup.  A tie group (equal 8-byte keys) hands the block to mode 1.
+        if (t < 256) {
+            const uint64_t m = __ballot(c != 0);
+            if (lane_id() == 0) {
+                present_out[(size_t)b * 8 + 2 * wave_id()] = (uint32_t)m;
+                present_out[(size_t)b * 8 + 2 * wave_id() + 1] = (uint32_t)(m >> 32);
+            }
+        }
+        const uint32_t nbat = pack_children(sh);
+        // buckets of one rotation are final (batches made only of them are
+        // dropped by pack_children): their BWT byte straight from the text
+        for (int i0 = t * 8; i0 < n; i0 += FT * 8) {
+            const uint2 wv = reinterpret_cast<const uint2*>(Tl)[i0 >> 3];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t v = ((k < 4 ? wv.x : wv.y) >> ((k & 3) * 8)) & 255u;
+                if (i0 + k < n && sh.hist[v] == 1u) {
+                    const uint32_t i = (uint32_t)(i0 + k), pos = sh.base[v];
+                    out[pos] = bwt_byte(Tl, n, i);
+                    if (i == 0) orig_out[b] = pos;
+                }
+            }
+        }
+        const int w = wave_id(), lane = lane_id();
+        constexpr int E = kSmall / 64;
+        Scratch s{};
+        s.sa = nullptr;
+        GroupSink sink{};
+        sink.redo = redo + b;
+        for (uint32_t k0 = 0; k0 < nbat;) {
+            if (t == 0) {
+                const uint32_t p0 = sh.bat_start[k0];
+                uint32_t k1 = k0 + 1;
+                while (k1 < nbat && sh.bat_start[k1] + (sh.bat_len[k1] & 0x7fffffffu) - p0 <= (uint32_t)kPassIdx) ++k1;
+                sh.bcast[0] = k1;
+                sh.bcast[1] = p0;
+                sh.bcast[2] = sh.bat_start[k1 - 1] + (sh.bat_len[k1 - 1] & 0x7fffffffu);
+            }
+            if (t < 256) L.th[t] = 0;
+            __syncthreads();
+            const uint32_t k1 = sh.bcast[0], pst = sh.bcast[1], pend = sh.bcast[2];
+            // stage the pass's rotation indices by first byte
+            for (int i0 = t * 8; i0 < n; i0 += FT * 8) {
+                const uint2 wv = reinterpret_cast<const uint2*>(Tl)[i0 >> 3];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t v = ((k < 4 ? wv.x : wv.y) >> ((k & 3) * 8)) & 255u;
+                    const uint32_t bs = sh.base[v];
+                    if (i0 + k < n && bs >= pst && bs < pend)
+                        L.u.pass.idx[bs - pst + atomicAdd(&L.th[v], 1u)] = (uint32_t)(i0 + k);
+                }
+            }
+            __syncthreads();
+            for (uint32_t k = k0 + (uint32_t)w; k < k1; k += FW) {
+                const uint32_t bl = uniform(sh.bat_len[k]);
+                const Seg seg{uniform(sh.bat_start[k]), bl & 0x7fffffffu};
+                BucketRef R{L.u.pass.base[w], L.u.pass.idx + (seg.start - pst)};
+                uint32_t pre[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const uint32_t g = (uint32_t)(e * 64 + lane);
+                    pre[e] = g < seg.len ? R.idx[g] : 0u;
+                }
+                wave_sort_bucket2(Tl, n, s, seg, bl >> 31, sink, out, orig_out + b, R, pre);
+            }
+            __syncthreads();
+            k0 = k1;
+        }
+        return;
+    }
     // ---- first-byte scatter, one 8192-rotation tile at a time (8 per thread)
     for (int tile0 = 0; tile0 < n; tile0 += FT * 8) {
         if (t < 256) L.th[t] = 0;
@@ -1500,6 +1610,8 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
         for (int e = 0; e < E; ++e) cur[e] = nxt[e];
     }
 }
+
+bool bwt_safree() { return kBwtSaFree; }
 
 // ---- kernel 2 (one launch per level, all blocks at once): every large
 // segment of the level queue is partitioned by one workgroup.  The last level

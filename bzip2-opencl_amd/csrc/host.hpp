@@ -82,6 +82,7 @@ struct Batch {
                                  // counter, [8 + d] level-d queue entries
     uint32_t* d_ngroups = nullptr;
     uint32_t* d_p2list = nullptr;
+    uint32_t* d_redo = nullptr;  // blocks the SA-free BWT pass hands back
     bz2mi::BwtSeg* d_groups = nullptr;
     // MTF / Huffman
     uint16_t* d_mtf = nullptr;
@@ -97,7 +98,7 @@ struct Batch {
     hipEvent_t evA = nullptr, evM = nullptr, evFree = nullptr;
 
     std::vector<void*> ptrs() const {
-        return {d_blocks, d_lens, d_crc, d_bwt, d_orig, d_sa, d_bcnt, d_ngroups, d_p2list, d_groups, d_mtf, d_mtflen, d_alpha, d_hist, d_present, d_seed, d_payload,
+        return {d_blocks, d_lens, d_crc, d_bwt, d_orig, d_sa, d_bcnt, d_ngroups, d_p2list, d_redo, d_groups, d_mtf, d_mtflen, d_alpha, d_hist, d_present, d_seed, d_payload,
                 d_pbits, d_offs};
     }
 };

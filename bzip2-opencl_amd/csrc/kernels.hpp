@@ -31,10 +31,14 @@ __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const ui
 // small buckets in one launch, the block's text held in LDS (1024 threads, one
 // workgroup per CU).  Large buckets still go to the level queue.
 constexpr int kBwtLdsText = 90112;
+bool bwt_safree();  // the SA-free pass is built in (mode 1 needed)
+// mode 0: blocks whose first-byte buckets are all small take the SA-free
+// LDS pass (redo[b] = 1 when a tie group needs the SA path); mode 1: the SA
+// path for the blocks with redo[b] set (redo zeroed before mode 0)
 __global__ void bwt_block_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                                  uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, BwtItem* lq,
                                  uint32_t* lcount, size_t lcap, uint32_t* present_out, uint64_t* tl,
-                                 uint32_t* tcount, size_t tcap);
+                                 uint32_t* tcount, size_t tcap, uint32_t* redo, int mode);
 __global__ void bwt_level_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                  uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,
                                  int S, const BwtItem* lin, const uint32_t* lin_count, BwtItem* lout,

@@ -3,12 +3,17 @@
 // messages (InputStream.hpp:84,114,121; BlockDecompressor.hpp:111,161,215,248,
 // 276; HuffmanStageDecoder.hpp:55; BitInputStream.hpp:47).
 //
-// Host decoder (decompression on the device is the next row of the plan).
-// Each block is decoded whole: Huffman tables -> MTF/RLE2 symbols -> inverse
-// BWT -> RLE1 expansion with the block CRC checked, then bytes are served from
-// the block buffer.  Blocks may be as large as the bzip2-standard digit x
-// 100,000 bytes, so streams of stock bzip2 and of bz2mi's 900 KB mode are read
-// too (the reference stops at digit x 10,000).
+// Decoding runs on the device (bz2mi_decompress, include/bz2mi.h; SURVEY 8(f)
+// row 1): at the first read the whole input is handed over and every block is
+// decoded at once (Huffman tables, MTF/RLE2, inverse BWT, RLE1 and the block /
+// stream CRCs), then bytes are served from the result.  Errors carry the
+// reference's messages; they surface at the first read() instead of after the
+// bytes of the blocks before the bad one.  Blocks may be as large as the
+// bzip2-standard digit x 100,000 bytes, so stock bzip2 streams and bz2mi's
+// 900 KB mode are read too (the reference stops at digit x 10,000).
+// BZ2MI_HOST_DECODER=1 selects the host decoder below instead (a block at a
+// time, the reference's structure: Huffman tables -> MTF/RLE2 symbols ->
+// inverse BWT -> RLE1 expansion with the block CRC checked).
 #ifndef INPUT_STREAM_HPP
 #define INPUT_STREAM_HPP
 
@@ -17,8 +22,13 @@
 #include <stdexcept>
 #include <vector>
 
+#include <cstdlib>
+#include <iterator>
+#include <string>
+
 #include "CRC32.hpp"
 #include "Config.hpp"
+#include "bz2mi.h"
 
 class InputStream
 {
@@ -91,6 +101,54 @@ private:
     {
         if (done_)
             return false;
+        if (!modeChosen_)
+        {
+            modeChosen_ = true;
+            const char *h = std::getenv("BZ2MI_HOST_DECODER");
+            host_ = h && *h && *h != '0';
+            if (!host_)
+                return refillDevice();
+        }
+        return refillHost();
+    }
+
+    // the whole input decoded on the device
+    bool refillDevice()
+    {
+        done_ = true;
+        std::vector<char> in((std::istreambuf_iterator<char>(in_)), std::istreambuf_iterator<char>());
+        int device = 0;
+        if (const char *d = std::getenv("BZ2MI_DEVICE"))
+            device = std::atoi(d);
+        bz2mi_dctx *d = bz2mi_dcreate(BLOCKSIZE_BZIP2, device);
+        if (!d)
+            throw std::runtime_error(std::string("bz2mi: ") + bz2mi_last_error());
+        block_.resize(in.size() * 4 + 65536);
+        size_t n = 0;
+        int rc = bz2mi_decompress(d, reinterpret_cast<const uint8_t *>(in.data()), in.size(), block_.data(),
+                                  block_.size(), &n);
+        if (rc == BZ2MI_ESPACE)
+        {
+            block_.resize(n);
+            rc = bz2mi_decompress(d, reinterpret_cast<const uint8_t *>(in.data()), in.size(), block_.data(),
+                                  block_.size(), &n);
+        }
+        const std::string err = rc == BZ2MI_OK ? std::string() : std::string(bz2mi_last_error());
+        bz2mi_ddestroy(d);
+        if (rc != BZ2MI_OK)
+        {
+            block_.clear();
+            throw std::runtime_error(err);
+        }
+        block_.resize(n);
+        pos_ = 0;
+        return !block_.empty();
+    }
+
+    bool refillHost()
+    {
+        if (done_)
+            return false;
         if (!started_)
             header();
         block_.clear();
@@ -100,7 +158,7 @@ private:
         {
             const uint32_t crc = decodeBlock();
             streamCRC_ = ((streamCRC_ << 1) | (streamCRC_ >> 31)) ^ crc;
-            return !block_.empty() || refill();
+            return !block_.empty() || refillHost();
         }
         if (m1 == static_cast<uint32_t>(STREAM_END_MARKER_1) && m2 == static_cast<uint32_t>(STREAM_END_MARKER_2))
         {
@@ -312,6 +370,8 @@ private:
     int have_ = 0;
     bool started_ = false;
     bool done_ = false;
+    bool modeChosen_ = false;  // device decoder unless BZ2MI_HOST_DECODER
+    bool host_ = false;
     int maxBlock_ = 0;
     uint32_t streamCRC_ = 0;
     std::vector<uint8_t> block_;

@@ -113,9 +113,17 @@ def harness(tmp_path_factory):
     src = d / "h.cpp"
     src.write_text(HARNESS)
     exe = d / "h"
+    _ensure_lib()
+    lib = os.path.dirname(LIB)
     subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", os.path.join(PKG, "include"),
-                    "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+                    "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe), "-L", lib, "-lbz2mi",
+                    "-Wl,-rpath," + lib], check=True)
     return str(exe)
+
+
+# the CPU tests run the mirror InputStream's host decoder (the device decoder
+# is its default; tests/test_app_gpu.py covers that path)
+HOST_DEC = dict(os.environ, BZ2MI_HOST_DECODER="1")
 
 
 def test_mirror_decoder_reads_golden_streams(harness, manifest, tmp_path):
@@ -124,7 +132,7 @@ def test_mirror_decoder_reads_golden_streams(harness, manifest, tmp_path):
         for st in e["streams"]:
             p = tmp_path / "x.bz2"
             p.write_bytes(golden_file(st["file"]))
-            out = subprocess.run([harness, "decode", str(p)], capture_output=True, check=True).stdout
+            out = subprocess.run([harness, "decode", str(p)], capture_output=True, check=True, env=HOST_DEC).stdout
             assert out == data, (name, st)
 
 
@@ -133,7 +141,7 @@ def test_mirror_decoder_rejects_corruption(harness, tmp_path):
     good[len(good) // 2] ^= 0x10
     p = tmp_path / "bad.bz2"
     p.write_bytes(bytes(good))
-    r = subprocess.run([harness, "decode", str(p)], capture_output=True)
+    r = subprocess.run([harness, "decode", str(p)], capture_output=True, env=HOST_DEC)
     assert r.returncode != 0  # std::runtime_error (CRC / table / format)
 
 
@@ -163,8 +171,8 @@ def test_reference_app_compiles_unchanged(tmp_path, manifest):
     data = golden_input("c1_text10k")
     src = tmp_path / "c1.bin.bz2"
     src.write_bytes(golden_file("oref/c1_text10k.s1.p10.bz2"))
-    r = subprocess.run([str(exe), str(src), "-d", "-k"], capture_output=True, cwd=tmp_path)
+    r = subprocess.run([str(exe), str(src), "-d", "-k"], capture_output=True, cwd=tmp_path, env=HOST_DEC)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "c1.bin").read_bytes() == data
-    r = subprocess.run([str(exe), str(src), "-c"], capture_output=True, text=True, cwd=tmp_path)
+    r = subprocess.run([str(exe), str(src), "-c"], capture_output=True, text=True, cwd=tmp_path, env=HOST_DEC)
     assert r.returncode == 0 and "Integrity check passed" in r.stdout

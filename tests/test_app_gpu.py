@@ -56,6 +56,28 @@ def test_app_small_and_empty(tmp_path):
         assert _compress(tmp_path, data, 9, 10, 100_000) == CpuRef().compress(data, 9, 10)
 
 
+def test_app_checks_fixtures_on_the_device(tmp_path, manifest):
+    """app.cpp -c / -d through the mirror InputStream, which decodes on the
+    device (bz2mi_decompress): every committed O_ref stream."""
+    for name, e in sorted(manifest["cases"].items()):
+        for st in e["streams"]:
+            p = tmp_path / (name + ".bin.bz2")
+            p.write_bytes(golden_file(st["file"]))
+            r = subprocess.run([APP, str(p), "-c"], capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0 and "Integrity check passed" in r.stdout, (st["file"], r.stderr)
+            r = subprocess.run([APP, str(p), "-d", "-k"], capture_output=True, timeout=120)
+            assert r.returncode == 0, r.stderr
+            out = tmp_path / (name + ".bin")
+            assert out.read_bytes() == golden_input(name), st["file"]
+            out.unlink()
+    bad = bytearray(golden_file("oref/text64k.s9.p10.bz2"))
+    bad[len(bad) // 2] ^= 0x10
+    p = tmp_path / "bad.bin.bz2"
+    p.write_bytes(bytes(bad))
+    r = subprocess.run([APP, str(p), "-c"], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+
+
 def test_app_round_trip_with_its_decoder(tmp_path):
     data = pin_input("mix2m75")
     z = _compress(tmp_path, data, 9, 10, 1 << 20)

@@ -4,7 +4,8 @@ cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${TAG:-ab}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest $R/tests/test_gpu.py $R/tests/test_shard.py $R/tests/test_pins.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS_FAILED; grep -E "FAIL|Error|assert" $O/tests.log | head -20; tail -20 $O/tests.log; exit 1; }
+TL=""; for t in ${TESTS:-tests/test_gpu.py tests/test_shard.py tests/test_pins.py}; do TL="$TL $R/$t"; done
+timeout -k 10 600 python -u -m pytest $TL -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS_FAILED; grep -E "FAIL|Error|assert" $O/tests.log | head -20; tail -20 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for v in tree $(ls $R/build_v 2>/dev/null); do
   lib=$R/build_v/$v/libbz2mi.so
