@@ -124,6 +124,26 @@ __device__ __forceinline__ uint8_t byte_at(const uint8_t* __restrict__ T, int n,
 // sits in element e of lane l): partners closer than E are in the same lane,
 // farther ones are lane ^ (j/E) reached with DPP / permlane moves.
 // WITH_LO: a 32-bit payload travels with each 64-bit key (not compared).
+// Every compare-exchange is branch-free: lane masks (which lanes are the
+// upper element of a pair, which sort descending) are per-stage constants,
+// the decision is one or two 64-bit compares combined on the scalar unit,
+// and the moves are selects.  Equal keys never duplicate a payload: an
+// exchange either swaps both elements or neither.
+template <int LJ>
+__device__ __forceinline__ void lane_pair(uint32_t v, uint32_t& a, uint32_t& b) {
+    // a = the pair's lower-lane element, b = its upper-lane element, in both lanes
+    if constexpr (LJ == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        a = r[0];
+        b = r[1];
+    } else {
+        static_assert(LJ == 32, "lane_pair: permlane distances");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        a = r[0];
+        b = r[1];
+    }
+}
+
 template <int E, bool WITH_LO, int K, int J>
 __device__ __forceinline__ void bitonic_stage(uint64_t (&key)[E], uint32_t (&lo)[E]) {
     const int lane = lane_id();
@@ -132,38 +152,60 @@ __device__ __forceinline__ void bitonic_stage(uint64_t (&key)[E], uint32_t (&lo)
         for (int e = 0; e < E; ++e) {
             const int pe = e ^ J;
             if (pe > e) {
-                const bool asc = ((lane * E + e) & K) == 0;
-                if ((key[e] > key[pe]) == asc) {
-                    const uint64_t tk = key[e];
-                    key[e] = key[pe];
-                    key[pe] = tk;
-                    if (WITH_LO) {
-                        const uint32_t tl = lo[e];
-                        lo[e] = lo[pe];
-                        lo[pe] = tl;
-                    }
+                // ascending pair: out of order when key[pe] < key[e]
+                bool sw;
+                if constexpr (K < E) {
+                    sw = ((e & K) == 0) ? key[pe] < key[e] : key[e] < key[pe];
+                } else if constexpr (!WITH_LO) {
+                    // no payload: equal keys are interchangeable, one compare
+                    sw = (key[pe] < key[e]) != (((lane * E) & K) != 0);
+                } else {
+                    const bool asc = ((lane * E) & K) == 0;
+                    const bool gt = key[pe] < key[e], lt = key[e] < key[pe];
+                    sw = asc ? gt : lt;
+                }
+                const uint64_t a = key[e], b = key[pe];
+                key[e] = sw ? b : a;
+                key[pe] = sw ? a : b;
+                if (WITH_LO) {
+                    const uint32_t la = lo[e], lb = lo[pe];
+                    lo[e] = sw ? lb : la;
+                    lo[pe] = sw ? la : lb;
                 }
             }
-
         }
     } else {
         constexpr int LJ = J / E;
-        const bool lower = (lane & LJ) == 0;
+        const bool up = (lane & LJ) != 0;             // upper element of the pair
+        const bool desc = ((lane * E) & K) != 0;      // (K >= 2E here: the same for every e)
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const uint64_t ok = ((uint64_t)xor_lanes<LJ>((uint32_t)(key[e] >> 32)) << 32) |
-                                xor_lanes<LJ>((uint32_t)key[e]);
-            const uint32_t ol = WITH_LO ? xor_lanes<LJ>(lo[e]) : 0u;
-            const bool asc = ((lane * E + e) & K) == 0;
-            // lower slot keeps the min when ascending, the max when descending;
-            // both comparisons strict so that equal keys keep their payloads
-            const bool lt = ok < key[e], gt = key[e] < ok;
-            const bool take = (lower == asc) ? lt : gt;
-            if (take) {
-                key[e] = ok;
-                if (WITH_LO) lo[e] = ol;
+            if constexpr (LJ >= 16) {
+                // both elements of the pair in both lanes; take b when
+                // (b < a) ^ up ^ desc
+                uint32_t ah, bh, al, bl, pa = 0, pb = 0;
+                lane_pair<LJ>((uint32_t)(key[e] >> 32), ah, bh);
+                lane_pair<LJ>((uint32_t)key[e], al, bl);
+                if (WITH_LO) lane_pair<LJ>(lo[e], pa, pb);
+                const uint64_t a = ((uint64_t)ah << 32) | al, b = ((uint64_t)bh << 32) | bl;
+                const bool tb = (b < a) != (up != desc);
+                key[e] = tb ? b : a;
+                if (WITH_LO) lo[e] = tb ? pb : pa;
+            } else {
+                const uint64_t ok = ((uint64_t)xor_lanes<LJ>((uint32_t)(key[e] >> 32)) << 32) |
+                                    xor_lanes<LJ>((uint32_t)key[e]);
+                const uint32_t ol = WITH_LO ? xor_lanes<LJ>(lo[e]) : 0u;
+                // lower lane keeps the min when ascending, upper the max
+                bool take;
+                if constexpr (!WITH_LO) {
+                    take = (ok < key[e]) != (up != desc);
+                } else {
+                    const bool lt = ok < key[e], gt = key[e] < ok;
+                    take = (up ? gt : lt) != desc;
+                }
+                key[e] = take ? ok : key[e];
+                if (WITH_LO) lo[e] = take ? ol : lo[e];
             }
-
         }
     }
 }
@@ -695,12 +737,186 @@ __device__ __forceinline__ uint64_t lds_key(const uint8_t* __restrict__ T, int n
     }
 }
 
+// ---- text in LDS: sorts on unique 57-bit keys and resolves ties in the wave.
+// A sort key is (6 text bytes at depth d) << 9 | item position, so keys are
+// unique and carry no payload (one 64-bit compare and two selects per
+// compare-exchange, a third of the cost of key + payload).  Items whose six
+// bytes tie are compacted to the front of their LDS index slice as
+// (index | destination slot << 17 | group head << 26) and sorted again on
+// (group's first slot << 49 | 5 bytes deeper << 9 | item), round after round,
+// until none tie; groups still tied at kMaxDepth go to the sink (tie kernel /
+// prefix doubling) with their SA entries written.  Requires n < 2^17.
+constexpr int kLdsKeyBytes = 6;   // bytes of the first round
+constexpr int kLdsTieBytes = 5;   // bytes of every tie round
+
+__device__ __forceinline__ uint64_t lane_next64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1), hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t lane_prev64(uint64_t v) {
+    return ((uint64_t)lane_prev((uint32_t)(v >> 32)) << 32) | lane_prev((uint32_t)v);
+}
+
+// one emission pass over sorted unique keys (prefix = key >> 9): final items
+// are written, tied ones compacted into idx[0, t) for the next round; returns t
+template <int E>
+__device__ __forceinline__ uint32_t lds_emit_round(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t base,
+                                                   uint32_t m, const uint64_t (&key)[E], const uint32_t (&src)[E],
+                                                   const uint32_t (&dst)[E], uint8_t* __restrict__ bwt,
+                                                   uint32_t* __restrict__ orig, uint32_t* __restrict__ idx) {
+    const int lane = lane_id();
+    uint64_t pk[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) pk[e] = key[e] >> 9;
+    const uint64_t before = lane_prev64(pk[E - 1]), after = lane_next64(pk[0]);
+    bool tie[E], head[E];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(lane * E + e);
+        const bool valid = g < m;
+        const bool tl = g > 0 && pk[e] == (e ? pk[e - 1] : before);
+        const bool tr = g + 1 < m && pk[e] == (e + 1 < E ? pk[e + 1 < E ? e + 1 : 0] : after);
+        tie[e] = valid && (tl || tr);
+        head[e] = tie[e] && !tl;
+        cnt += tie[e];
+        if (valid && !tie[e]) {
+            const uint32_t i = src[e], pos = base + dst[e];
+            if (s.sa) s.sa[pos] = i;
+            bwt[pos] = bwt_byte(T, n, i);
+            if (i == 0) *orig = pos;
+        }
+    }
+    const uint32_t inc = wave_incl_sum(cnt);
+    const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    if (t) {
+        __builtin_amdgcn_wave_barrier();  // every lane has read idx[] (caller) before it is rewritten
+        uint32_t o = inc - cnt;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (tie[e]) idx[o++] = src[e] | (dst[e] << 17) | ((uint32_t)head[e] << 26);
+        __builtin_amdgcn_wave_barrier();
+    }
+    return t;
+}
+
+// tie round over the t compacted items idx[0, t) at depth D
+template <int E>
+__device__ __forceinline__ uint32_t lds_tie_round(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t base,
+                                               uint32_t t, uint32_t D, uint8_t* __restrict__ bwt,
+                                               uint32_t* __restrict__ orig, uint32_t* __restrict__ idx) {
+    const int lane = lane_id();
+    uint64_t key[E];
+    uint32_t gs[E], run = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t q = (uint32_t)(lane * E + e);
+        const uint32_t w = q < t ? idx[q] : 0u;
+        if (w >> 26) run = (w >> 17) & 511u;  // group heads carry increasing slots
+        gs[e] = run;
+        key[e] = q < t ? (uint64_t)(w & 0x1ffffu) : ~0ull;  // index, keyed below
+    }
+    const uint32_t carry = lane_prev(wave_incl_max(run), 0u);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t q = (uint32_t)(lane * E + e);
+        if (q < t) {
+            const uint32_t g = gs[e] > carry ? gs[e] : carry;
+            const uint32_t p = (uint32_t)(((uint64_t)key[e] + D) % (uint32_t)n);
+            key[e] = ((uint64_t)g << 49) | ((load8(T, n, p) >> 24) << 9) | q;
+        }
+    }
+    uint32_t dummy[E];
+    wave_bitonic<E, false>(key, dummy);
+    uint32_t src[E], dst[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t r = (uint32_t)(lane * E + e);
+        src[e] = r < t ? idx[key[e] & 511u] & 0x1ffffu : 0u;
+        dst[e] = r < t ? (idx[r] >> 17) & 511u : 0u;
+    }
+    return lds_emit_round<E>(T, n, s, base, t, key, src, dst, bwt, orig, idx);
+}
+
+__device__ __forceinline__ uint32_t lds_tie_round_any(const uint8_t* T, int n, Scratch& s, uint32_t base, uint32_t t,
+                                                      uint32_t D, uint8_t* bwt, uint32_t* orig, uint32_t* idx) {
+    if (t <= 64) return lds_tie_round<1>(T, n, s, base, t, D, bwt, orig, idx);
+    if (t <= 128) return lds_tie_round<2>(T, n, s, base, t, D, bwt, orig, idx);
+    if (t <= 256) return lds_tie_round<4>(T, n, s, base, t, D, bwt, orig, idx);
+    return lds_tie_round<8>(T, n, s, base, t, D, bwt, orig, idx);
+}
+
+// groups still tied at the depth limit: SA entries written, groups to the sink
+__device__ __forceinline__ void lds_tie_spill(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t base,
+                                           uint32_t t, uint32_t D, const GroupSink& sink,
+                                           const uint32_t* __restrict__ idx) {
+    for (uint32_t q0 = 0; q0 < t; q0 += 64) {
+        const uint32_t q = q0 + (uint32_t)lane_id();
+        const uint32_t w = q < t ? idx[q] : 0u;
+        const uint32_t slot = (w >> 17) & 511u;
+        if (q < t && s.sa) s.sa[base + slot] = w & 0x1ffffu;
+        uint32_t len = 0;
+        if (q < t && (w >> 26)) {
+            len = 1;
+            while (q + len < t && !(idx[q + len] >> 26)) ++len;
+        }
+        sink.push_agg(len >= 2, Seg{base + slot, len}, D);
+    }
+}
+
+template <int E, class BL>
+__device__ __forceinline__ uint32_t wave_sort_lds_text(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t start,
+                                                   uint32_t b0, uint32_t m, uint32_t d, const GroupSink& sink,
+                                                   uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
+                                                   BL& L) {
+    const int lane = lane_id();
+    uint32_t* idx = L.idx + b0;
+    uint64_t key[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(lane * E + e);
+        if (g < m) {
+            uint32_t p = (idx[g] & 0xffffffu) + d;
+            if (p >= (uint32_t)n) p %= (uint32_t)n;
+            key[e] = ((load8(T, n, p) >> (64 - 8 * kLdsKeyBytes)) << 9) | g;
+        } else {
+            key[e] = ~0ull;
+        }
+    }
+    uint32_t dummy[E];
+    wave_bitonic<E, false>(key, dummy);
+    uint32_t src[E], dst[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(lane * E + e);
+        src[e] = g < m ? idx[key[e] & 511u] & 0xffffffu : 0u;
+        dst[e] = g;
+    }
+    return lds_emit_round<E>(T, n, s, start + b0, m, key, src, dst, bwt, orig, idx);
+}
+
+// the tie rounds after a first round left t items tied (depth d + kLdsKeyBytes)
+__device__ __forceinline__ void lds_ties(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t base, uint32_t t,
+                                         uint32_t d, const GroupSink& sink, uint8_t* __restrict__ bwt,
+                                         uint32_t* __restrict__ orig, uint32_t* __restrict__ idx) {
+    uint32_t D = d + kLdsKeyBytes;
+    while (t) {
+        if (D + kLdsTieBytes > (uint32_t)kMaxDepth) {
+            lds_tie_spill(T, n, s, base, t, D, sink, idx);
+            return;
+        }
+        t = uniform(lds_tie_round_any(T, n, s, base, t, D, bwt, orig, idx));
+        D += kLdsTieBytes;
+    }
+}
+
 // wave sort of LDS items [b0, b0+m) (m <= 64*E), emitted at seg.start + b0
 template <int E, class BL>
 __device__ __forceinline__ void wave_sort_lds(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t start,
                                               uint32_t b0, uint32_t m, uint32_t d, const GroupSink& sink,
                                               uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
-                                              const BL& L) {
+                                              BL& L) {
+    static_assert(BL::kKeys, "LDS-text buckets sort with wave_sort_lds_text");
     const int lane = lane_id();
     uint64_t key[E];
     uint32_t lo[E];
@@ -717,11 +933,20 @@ template <class BL>
 __device__ __forceinline__ void wave_sort_lds_any(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t start,
                                                uint32_t b0, uint32_t m, uint32_t d, const GroupSink& sink,
                                                uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
-                                               const BL& L) {
-    if (m <= 64) wave_sort_lds<1, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
-    else if (m <= 128) wave_sort_lds<2, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
-    else if (m <= 256) wave_sort_lds<4, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
-    else wave_sort_lds<8, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+                                               BL& L) {
+    if constexpr (!BL::kKeys) {
+        uint32_t t;
+        if (m <= 64) t = wave_sort_lds_text<1, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+        else if (m <= 128) t = wave_sort_lds_text<2, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+        else if (m <= 256) t = wave_sort_lds_text<4, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+        else t = wave_sort_lds_text<8, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+        if (t) lds_ties(T, n, s, start + b0, t, d, sink, bwt, orig, L.idx + b0);
+    } else {
+        if (m <= 64) wave_sort_lds<1, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+        else if (m <= 128) wave_sort_lds<2, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+        else if (m <= 256) wave_sort_lds<4, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+        else wave_sort_lds<8, BL>(T, n, s, start, b0, m, d, sink, bwt, orig, L);
+    }
 }
 
 // `pre`: the batch's SA entries, loaded ahead by the caller (entry e*64+lane in pre[e])
