@@ -609,7 +609,7 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     c->S = unit * level;
     c->device = device;
     c->stride = ((size_t)c->S + 16 + 63) & ~(size_t)63;
-    c->mtf_stride = ((size_t)c->S + 2 + 31) & ~(size_t)31;
+    c->mtf_stride = ((size_t)c->S + 10 + 31) & ~(size_t)31;  // (+8: room for 16-byte reads past a group)
     {
         const size_t S = (size_t)c->S;
         const size_t bits = 24 + 272 + 18 + (S / 50 + 1) * 6 + 6 * (5 + 258 * 39) + (S + 1) * 20;

@@ -423,6 +423,16 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
     uint32_t g = 0, gleft = kGroupRun, ns = 0, status = 0;
     uint32_t tbase = (uint32_t)sg[0] << kLutBits;
     uint32_t nsel1 = nsel > 1 ? sg[1] : 0u;  // next group's table, loaded ahead
+    // symbols leave in 16-byte stores of 8: a 128-bit shift register (the
+    // newest symbol enters at the top), stored when 8 have entered -- one
+    // store per 8 symbols instead of a 2-byte store per symbol
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    auto push = [&](uint32_t v) {
+        a0 = __builtin_amdgcn_alignbit(a1, a0, 16);
+        a1 = __builtin_amdgcn_alignbit(a2, a1, 16);
+        a2 = __builtin_amdgcn_alignbit(a3, a2, 16);
+        a3 = (a3 >> 16) | (v << 16);
+    };
     for (;;) {
         const uint32_t e = L[tbase + br.peek(kLutBits)];
         uint32_t sym, len;
@@ -442,7 +452,8 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
             status = kDecData;
             break;
         }
-        so[ns++] = (uint16_t)sym;
+        push(sym);
+        if ((++ns & 7u) == 0) *reinterpret_cast<uint4*>(so + ns - 8) = make_uint4(a0, a1, a2, a3);
         if (sym == eob) break;
         if (ns >= ns_max) {
             status = kDecSize;
@@ -457,6 +468,10 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
             nsel1 = g + 1 < nsel ? sg[g + 1] : 0u;
             gleft = kGroupRun;
         }
+    }
+    if (ns & 7u) {  // the last partial 8 (zeros after it: the stride is a multiple of 64 symbols)
+        for (uint32_t q = ns & 7u; q < 8; ++q) push(0u);
+        *reinterpret_cast<uint4*>(so + (ns & ~7u)) = make_uint4(a0, a1, a2, a3);
     }
     info->status = status;
     info->nsym = ns;

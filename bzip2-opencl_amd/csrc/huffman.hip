@@ -40,7 +40,14 @@ namespace {
 #endif
 constexpr int NT = BZ2MI_HUF_NT;
 constexpr int NW = NT / 64;
-constexpr int kTileSyms = 8 * NT;                    // symbols per data tile
+// BZ2MI_HUF_TS: symbols per thread of a data tile (8 or 4; 4 halves the
+// output window, so the workgroup fits 8 per CU)
+#ifndef BZ2MI_HUF_TS
+#define BZ2MI_HUF_TS 8
+#endif
+constexpr int TS = BZ2MI_HUF_TS;
+static_assert(TS == 8 || TS == 4, "tile symbols per thread");
+constexpr int kTileSyms = TS * NT;                   // symbols per data tile
 constexpr int kWinWords = kTileSyms * kMaxCodeLen / 32 + 2;
 
 struct HufShared {
@@ -116,20 +123,65 @@ __device__ __forceinline__ int mod_len(int x, int len) {
     return x % len;
 }
 
-__device__ int ha_first(const WaveList& a, int len, int i, int nodesToMove) {
+// first() (kernel.cpp:2661-2686) with every probe of its exponential and
+// binary searches answered from bit masks: am holds mod_len of every entry,
+// one compare per register gives the predicate "parent above limit" for all
+// 320 entries at once (five 64-bit masks in SGPRs), and the searches run on
+// the scalar unit with the reference's exact probe sequence -- no readlane
+// round trips per probe, and no assumption that the predicate is monotone.
+__device__ __forceinline__ int ha_first(const WaveList& am, int len, int i, int nodesToMove) {
+    (void)len;
     const int limit = i;
+    const uint64_t p0 = __ballot(am.r0 > limit), p1 = __ballot(am.r1 > limit), p2 = __ballot(am.r2 > limit);
+    const uint64_t p3 = __ballot(am.r3 > limit), p4 = __ballot(am.r4 > limit);
+    auto P = [&](int j) -> bool {
+        const int q = j >> 6;
+        const uint64_t m = q == 0 ? p0 : q == 1 ? p1 : q == 2 ? p2 : q == 3 ? p3 : p4;
+        return (m >> (j & 63)) & 1ull;
+    };
+    // Fast path: when the predicate over [lo, limit] is true on a suffix that
+    // reaches `limit` (the parent pointers are nondecreasing, so it is, bar
+    // ~3% of calls), the searches end at the suffix's first index.  Checked
+    // against first() on 47M calls of random allocations; anything else
+    // takes the probe sequence below.
+    const int lo = nodesToMove > 0 ? nodesToMove : 0;
+    if (lo <= limit && P(limit)) {
+        int hf = -1, lt = 1 << 30;
+#pragma unroll
+        for (int w = 4; w >= 0; --w) {
+            const uint64_t pw = w == 0 ? p0 : w == 1 ? p1 : w == 2 ? p2 : w == 3 ? p3 : p4;
+            const int a = lo - 64 * w, b = limit - 64 * w;
+            uint64_t rng = 0;
+            if (b >= 0 && a <= 63) rng = (b >= 63 ? ~0ull : ((2ull << b) - 1ull)) & (a <= 0 ? ~0ull : (~0ull << a));
+            const uint64_t f = ~pw & rng, tr = pw & rng;
+            if (hf < 0 && f) hf = 64 * w + 63 - __clzll((long long)f);
+            if (tr) lt = 64 * w + __builtin_ctzll(tr);
+        }
+        if (hf < lt) return hf < 0 ? lo : hf + 1;
+    }
     int k = len - 2;
-    while (i >= nodesToMove && mod_len(a.get(i), len) > limit) {
+    while (i >= nodesToMove && P(i)) {
         k = i;
         i -= (limit - i + 1);
     }
     if (i < nodesToMove - 1) i = nodesToMove - 1;
     while (k > i + 1) {
         const int t = (i + k) >> 1;
-        if (mod_len(a.get(t), len) > limit) k = t;
+        if (P(t)) k = t;
         else i = t;
     }
     return k;
+}
+
+// the entries' values mod len (first()'s `array[i] % length`), lane-parallel
+__device__ __forceinline__ WaveList mod_list(const WaveList& a, int len) {
+    WaveList m;
+    m.r0 = mod_len(a.r0, len);
+    m.r1 = mod_len(a.r1, len);
+    m.r2 = mod_len(a.r2, len);
+    m.r3 = mod_len(a.r3, len);
+    m.r4 = mod_len(a.r4, len);
+    return m;
 }
 
 // Phase 1 of the allocator: the extended parent pointers of the in-place
@@ -191,16 +243,18 @@ __device__ void ha_parents(int* A, int* IW, int* M, int len) {
 // Phase 2 (kernel.cpp:2714-2806): depths from the parent pointers, limited to
 // kMaxCodeLen, written from the top of the array.
 __device__ void ha_depths(WaveList& a, int len) {
+    WaveList am = mod_list(a, len);  // kept equal to mod_len of every entry of a
     int r = len - 2;
-    for (int d = 1; d < kMaxCodeLen - 1 && r > 1; d++) r = ha_first(a, len, r - 1, 0);
+    for (int d = 1; d < kMaxCodeLen - 1 && r > 1; d++) r = ha_first(am, len, r - 1, 0);
     if (mod_len(a.get(0), len) >= r) {
         int firstNode = len - 2, nextNode = len - 1;
         for (int d = 1, avail = 2; avail > 0 && d < 64; d++) {
             const int lastNode = firstNode;
-            firstNode = ha_first(a, len, lastNode - 1, 0);
+            firstNode = ha_first(am, len, lastNode - 1, 0);
             const int cnt = avail - (lastNode - firstNode);
             if (cnt > 0) {
                 a.fill(nextNode - cnt, nextNode, d);
+                am.fill(nextNode - cnt, nextNode, mod_len(d, len));
                 nextNode -= cnt;
             }
             avail = (lastNode - firstNode) << 1;
@@ -212,7 +266,7 @@ __device__ void ha_depths(WaveList& a, int len) {
         int left = (insertDepth == 1) ? r - 2 : r;
         for (int avail = d << 1; avail > 0 && d < 64; d++) {
             const int lastNode = firstNode;
-            if (firstNode > r) firstNode = ha_first(a, len, lastNode - 1, r);
+            if (firstNode > r) firstNode = ha_first(am, len, lastNode - 1, r);
             int off = 0;
             if (d >= insertDepth) {
                 const int cap = 1 << (d - insertDepth);
@@ -224,6 +278,7 @@ __device__ void ha_depths(WaveList& a, int len) {
             const int cnt = avail - (lastNode - firstNode + off);
             if (cnt > 0) {
                 a.fill(nextNode - cnt, nextNode, d);
+                am.fill(nextNode - cnt, nextNode, mod_len(d, len));
                 nextNode -= cnt;
             }
             left -= off;
@@ -275,7 +330,7 @@ __device__ __forceinline__ void wave_bitonic32(uint32_t (&key)[8]) {
 // code lengths of table q from sh.u.opt.tf[q] (generateHuffmanCodeLengths,
 // kernel.cpp:2835-2857) on one wave: sort the unique keys (freq << 9) | symbol,
 // run the allocator on the sorted frequencies, scatter depths to symbols
-__device__ void build_table(HufShared& sh, int q, int alpha) {
+__device__ void build_table(HufShared& sh, int q, int alpha, bool stamp = false) {
     const int lane = lane_id();
     int* tf = sh.u.opt.tf[q];
     int* A = sh.u.opt.work[q];
@@ -289,14 +344,17 @@ __device__ void build_table(HufShared& sh, int q, int alpha) {
     else if (alpha <= 128) wave_bitonic32<2>(key);
     else if (alpha <= 256) wave_bitonic32<4>(key);
     else wave_bitonic32<8>(key);
+    BZ2MI_PHASE(g_huf_phase, 13, stamp);
 #pragma unroll
     for (int e = 0; e < 5; ++e)
         if (e * 64 + lane < alpha) A[e * 64 + lane] = (int)(key[e] >> 9);
     WaveList a;
     if (alpha > 2) {
         ha_parents(A, tf, sh.mrg[wave_id()], alpha);  // (tf[q] is free: keys are in registers)
+        BZ2MI_PHASE(g_huf_phase, 14, stamp);
         a.load(A, alpha);
         ha_depths(a, alpha);
+        BZ2MI_PHASE(g_huf_phase, 15, stamp);
     } else {
         a.load(A, alpha);
         a.fill(-1, alpha - 1, 1);  // (alpha >= 3 in practice: RUNA, RUNB, EOB)
@@ -308,9 +366,9 @@ __device__ void build_table(HufShared& sh, int q, int alpha) {
 }
 
 // code lengths of every table, table q on wave q%NW
-__device__ void build_lengths(HufShared& sh, int T, int alpha) {
+__device__ void build_lengths(HufShared& sh, int T, int alpha, bool stamp = false) {
     for (int q = 0; q < T; ++q)
-        if (my_table(q)) build_table(sh, q, alpha);
+        if (my_table(q)) build_table(sh, q, alpha, stamp && q == 0);
     __syncthreads();
 }
 
@@ -484,7 +542,7 @@ __global__ __launch_bounds__(NT, BZ2MI_HUF_WGS) void huffman_kernel(
         }
         __syncthreads();
         BZ2MI_PHASE(g_huf_phase, 2 + 2 * (3 - it), stamp);
-        build_lengths(sh, T, alpha);
+        build_lengths(sh, T, alpha, stamp && it == 0);
         BZ2MI_PHASE(g_huf_phase, 3 + 2 * (3 - it), stamp);
     }
 
@@ -641,24 +699,32 @@ __global__ __launch_bounds__(NT, BZ2MI_HUF_WGS) void huffman_kernel(
     uint64_t bit0 = data0;  // stream position of the current tile
     int cur = 0;
     for (int base = 0; base < m; base += kTileSyms) {
-        const int i0 = base + 8 * t;
-        uint32_t sym[8];
-        if (i0 + 8 <= m) {
-            const uint4 v = *reinterpret_cast<const uint4*>(X + i0);
-            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+        const int i0 = base + TS * t;
+        uint32_t sym[TS];
+        if (i0 + TS <= m) {
+            if constexpr (TS == 8) {
+                const uint4 v = *reinterpret_cast<const uint4*>(X + i0);
+                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                sym[2 * k] = vv[k] & 0xffffu;
-                sym[2 * k + 1] = vv[k] >> 16;
+                for (int k = 0; k < 4; ++k) {
+                    sym[2 * k] = vv[k] & 0xffffu;
+                    sym[2 * k + 1] = vv[k] >> 16;
+                }
+            } else {
+                const uint2 v = *reinterpret_cast<const uint2*>(X + i0);
+                sym[0] = v.x & 0xffffu;
+                sym[1] = v.x >> 16;
+                sym[2] = v.y & 0xffffu;
+                sym[3] = v.y >> 16;
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) sym[k] = i0 + k < m ? X[i0 + k] : 0u;
+            for (int k = 0; k < TS; ++k) sym[k] = i0 + k < m ? X[i0 + k] : 0u;
         }
-        uint32_t cs[8];
+        uint32_t cs[TS];
         uint32_t mybits = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < TS; ++k) {
             const int i = i0 + k;
             cs[k] = i < m ? sh.u.out.codes[sel[(unsigned)i / kGroupRun]][sym[k]] : 0u;
             mybits += cs[k] >> 24;
@@ -673,7 +739,7 @@ __global__ __launch_bounds__(NT, BZ2MI_HUF_WGS) void huffman_kernel(
             int nacc = (int)(p & 31);
             uint64_t acc = 0;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < TS; ++k) {
                 const int L = (int)(cs[k] >> 24);
                 acc |= ((uint64_t)(cs[k] & 0xffffffu) << (63 - L) << 1) >> nacc;
                 nacc += L;

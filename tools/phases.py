@@ -27,6 +27,9 @@ for k, name in [(0, "huffman"), (1, "bwt"), (2, "mtf"), (3, "fe_chain windows")]
     n_ = max(i for i in range(16) if v[i]) if any(v) else 0
     print(name, "rc", r, "us:", [round((v[i + 1] - v[i]) / 100.0, 1) for i in range(n_) if v[i] and v[i + 1]],
           "total", round((v[n_] - v[0]) / 100.0, 1) if n_ else None)
+L.bz2mi_debug_phases(0, buf)
+v = list(buf)
+print("huffman raw us from slot 0:", [round((x - v[0]) / 100.0, 1) if x else None for x in v])
 L.bz2mi_debug_phases(3, buf)
 v = list(buf)
 print("fe sums (us): table", v[6] / 100.0, "chase", v[7] / 100.0, "bnd", v[8] / 100.0, "slow", v[9] / 100.0, "ends out", v[10], "mid", v[11])

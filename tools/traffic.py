@@ -15,9 +15,11 @@ import sys
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/round"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01_traffic.json"
 steps = 2
+suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # e.g. "_random" for tools/r2_round.sh
+workload = sys.argv[4] if len(sys.argv) > 4 else "C2"
 per = collections.defaultdict(lambda: {"fetch_bytes": 0.0, "write_bytes": 0.0, "dispatches": 0})
 for counter, sub, scale in (("FETCH_SIZE", "pmc_fetch", 2.0), ("WRITE_SIZE", "pmc_write", 1.0)):
-    for r in csv.DictReader(open(f"{src}/{sub}/run_counter_collection.csv")):
+    for r in csv.DictReader(open(f"{src}/{sub}{suffix}/run_counter_collection.csv")):
         if "bz2mi::" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
             continue
         k = r["Kernel_Name"].split("(")[0].replace("bz2mi::", "")
@@ -27,8 +29,8 @@ for counter, sub, scale in (("FETCH_SIZE", "pmc_fetch", 2.0), ("WRITE_SIZE", "pm
             per[k]["dispatches"] += 1
 stages = {"front": ["fe_"], "bwt": ["bwt_"], "mtf": ["mtf_kernel"], "huffman": ["huffman_kernel"],
           "assemble": ["assemble", "offsets_dev", "advance"]}
-out = {"command": "python3 bench.py --no-cpu --no-verify --steps 1 --warmup 1 (C2, 1 GiB random, -9, p=10)",
-       "workload": "C2", "note": "bytes per compression of the 1 GiB input; FETCH_SIZE x2 (gfx950 correction)",
+out = {"command": "python3 bench.py --no-cpu --no-verify --steps 1 --warmup 1 [--data ...] (1 GiB, -9, p=10)",
+       "workload": workload, "note": "bytes per compression of the 1 GiB input; FETCH_SIZE x2 (gfx950 correction)",
        "kernels": {k: {a: round(b) for a, b in v.items()} for k, v in sorted(per.items())},
        "stages": {}}
 for st, pre in stages.items():
