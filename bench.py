@@ -51,20 +51,22 @@ def ensure_built():
         subprocess.run(["make", "-C", PKG, "-j8"], check=True, stdout=subprocess.DEVNULL)
 
 
-TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r01_traffic.json")
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r02_traffic_{data}.json")
 
 
 def stage_traffic(args, stage):
     """HBM-side bytes per launch of `stage` from the committed rocprofv3 --pmc
     passes of this same command (tools/round_profile.sh -> tools/traffic.py:
     FETCH_SIZE x2 per the gfx950 note of MI355X_MICROARCH.md, + WRITE_SIZE).
-    Only for the workload those passes ran (C2 at the default level/p/unit)."""
-    if args.data != "random" or args.mib != 1024 or args.level != 9 or args.parallel != 10 or args.unit != 10000:
+    Only for the workloads those passes ran (1 GiB of --data random/text at the
+    default level/p/unit; tools/r2_round.sh)."""
+    if args.mib != 1024 or args.level != 9 or args.parallel != 10 or args.unit != 10000:
         return None, None
+    path = TRAFFIC_PROFILE.format(data=args.data)
     try:
-        with open(TRAFFIC_PROFILE) as f:
+        with open(path) as f:
             prof = json.load(f)
-        return int(prof["stages"][stage]["traffic_bytes"]), os.path.relpath(TRAFFIC_PROFILE, REPO)
+        return int(prof["stages"][stage]["traffic_bytes"]), os.path.relpath(path, REPO)
     except (OSError, KeyError, ValueError):
         return None, None
 

@@ -253,6 +253,7 @@ int ensure_front(FrontBufs& f, int S, size_t n) {
     if ((r = dalloc(&f.d_dmap, cap + cap / 4 + 4096))) return r;
     if ((r = dalloc(&f.d_summ, nc + 1))) return r;
     if ((r = dalloc(&f.d_rsb, nc + 2))) return r;
+    if ((r = dalloc(&f.d_agg, nc / kFeScanTile + 2))) return r;
     if ((r = dalloc(&f.d_ccost, nc + 1))) return r;
     if ((r = dalloc(&f.d_fc, nc + 2))) return r;
     if ((r = dalloc(&f.d_bnd, maxb + 2))) return r;
@@ -275,10 +276,13 @@ int enqueue_front_scan(FrontBufs& f, const uint8_t* d_x, size_t n, hipStream_t s
     const uint64_t nc = (n + kFeChunk - 1) / kFeChunk;
     const dim3 g4((unsigned)((nc + 3) / 4));
     hipLaunchKernelGGL(fe_summary_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, f.d_summ);
-    hipLaunchKernelGGL(fe_runscan_kernel, dim3(1), dim3(kFeScanThreads), 0, s, f.d_summ, nc, f.d_rsb);
+    const dim3 gs((unsigned)((nc + kFeScanTile - 1) / kFeScanTile));
+    for (int pass = 0; pass < 2; ++pass)
+        hipLaunchKernelGGL(fe_runscan_kernel, gs, dim3(kFeScanThreads), 0, s, f.d_summ, nc, f.d_rsb, f.d_agg, pass);
     hipLaunchKernelGGL(fe_cost_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, f.d_summ, f.d_rsb, f.d_cost,
                        f.d_ccost);
-    hipLaunchKernelGGL(fe_costscan_kernel, dim3(1), dim3(kFeScanThreads), 0, s, f.d_ccost, nc, f.d_fc);
+    for (int pass = 0; pass < 2; ++pass)
+        hipLaunchKernelGGL(fe_costscan_kernel, gs, dim3(kFeScanThreads), 0, s, f.d_ccost, nc, f.d_fc, f.d_agg, pass);
     hipLaunchKernelGGL(fe_dmap_kernel, g4, dim3(256), 0, s, d_x, f.d_cost, (uint64_t)n, nc, f.d_fc, f.d_dmap);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("front-scan");

@@ -392,17 +392,20 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
                                                      const uint8_t* __restrict__ tabs, uint32_t nids, uint32_t smax,
                                                      uint16_t* __restrict__ syms, size_t sym_stride,
                                                      DecBlockInfo* __restrict__ infos) {
-    __shared__ uint16_t lut[kSymBlocks][kMaxTables * (1 << kLutBits)];
+    // the lookup tables (the table layout's first kTabLimit bytes) of the
+    // wave's blocks; the long-code limit / base arrays stay in global memory
+    // (staged too they cost occupancy: measured 80 -> 104 ms per GiB)
+    static_assert(kTabLimit == kMaxTables * (1 << kLutBits) * 2, "table layout");
+    __shared__ uint32_t tabl[kSymBlocks][kTabLimit / 4];
     const int lane = lane_id();
     const uint32_t k0 = blockIdx.x * kSymBlocks;
-    // stage the lookup tables of this wave's blocks
+    // stage the tables of this wave's blocks
     for (int b = 0; b < kSymBlocks; ++b) {
         if (k0 + b >= nids) break;
         const uint32_t st = uniform(infos[k0 + b].status);
         if (st) continue;
         const uint32_t* s32 = reinterpret_cast<const uint32_t*>(tabs + (size_t)(k0 + b) * kTabBytes);
-        uint32_t* d32 = reinterpret_cast<uint32_t*>(&lut[b][0]);
-        for (int i = lane; i < kMaxTables * (1 << kLutBits) / 2; i += 64) d32[i] = s32[i];
+        for (int i = lane; i < (int)(kTabLimit / 4); i += 64) tabl[b][i] = s32[i];
     }
     __syncthreads();
     const uint32_t k = k0 + (uint32_t)lane;
@@ -410,12 +413,13 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
     DecBlockInfo* info = infos + k;
     if (info->status) return;
     const uint8_t* tb = tabs + (size_t)k * kTabBytes;
+    const uint8_t* tl = reinterpret_cast<const uint8_t*>(&tabl[lane][0]);
     const int32_t* lim = reinterpret_cast<const int32_t*>(tb + kTabLimit);
     const int32_t* bas = reinterpret_cast<const int32_t*>(tb + kTabBase);
     const uint16_t* per = reinterpret_cast<const uint16_t*>(tb + kTabPerm);
     const uint8_t* sg = tb + kTabSel;
     const uint32_t nsel = info->nsel, eob = info->alpha + 1;
-    const uint16_t* L = &lut[lane][0];
+    const uint16_t* L = reinterpret_cast<const uint16_t*>(tl);
     BitReader br;
     br.init(in, n, info->data_bit);
     uint16_t* so = syms + (size_t)k * sym_stride;
@@ -549,8 +553,25 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
         cnt += run;
         inrun = false;
     };
+    // the chunk's symbols arrive 8 at a time (16-byte loads), the next 8
+    // loaded while the current 8 are decoded: a load per symbol, waited on
+    // at once, was a memory latency per symbol
+    const uint32_t glast = (uint32_t)(sym_stride - 8);  // last 8-group of the row (the stride is a multiple of 64)
+    uint32_t gcur = a & ~7u;
+    uint4 qc = make_uint4(0, 0, 0, 0), qn = make_uint4(0, 0, 0, 0);
+    if (a < b) {
+        qc = *reinterpret_cast<const uint4*>(so + gcur);
+        qn = *reinterpret_cast<const uint4*>(so + min(gcur + 8, glast));
+    }
     for (uint32_t p = a; p < b; ++p) {
-        const uint32_t s = so[p];
+        if (p >= gcur + 8) {
+            gcur += 8;
+            qc = qn;
+            qn = *reinterpret_cast<const uint4*>(so + min(gcur + 8, glast));
+        }
+        const uint32_t wq = (p >> 1) & 3u;
+        const uint32_t dw = wq == 0 ? qc.x : wq == 1 ? qc.y : wq == 2 ? qc.z : qc.w;
+        const uint32_t s = (p & 1u) ? dw >> 16 : dw & 0xffffu;
         if (s <= 1) {  // RUNA / RUNB digit
             if (!inrun) {
                 inrun = true;
@@ -646,9 +667,11 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
         const uint32_t ca = uniform((uint32_t)__builtin_amdgcn_readlane((int)a, c));
         const uint32_t cb = uniform((uint32_t)__builtin_amdgcn_readlane((int)b, c));
         uint32_t o = uniform((uint32_t)__builtin_amdgcn_readlane((int)cbase, c));
+        uint32_t xn = ca + (uint32_t)lane < cb ? tv[ca + lane] : 0u;  // one 64-symbol step ahead
         for (uint32_t p0 = ca; p0 < cb; p0 += 64) {
-            const uint32_t p = p0 + (uint32_t)lane;
-            const uint32_t x = p < cb ? tv[p] : 0u;
+            const uint32_t x = xn;
+            const uint32_t pn = p0 + 64 + (uint32_t)lane;
+            xn = pn < cb ? tv[pn] : 0u;
             const uint32_t n1 = x >> 8;
             const uint32_t inc1 = wave_incl_sum(n1);
             uint32_t q = o + inc1 - n1;
@@ -685,19 +708,27 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
 // origPtr), walk to the next start row (pass A: segment lengths and
 // successors), thread 0 chains the segments from walker 0, and the walkers
 // walk again writing their segment's bytes (pass B).
+constexpr int kIT = kDecIbwtThreads;  // threads per inverse-BWT workgroup
+constexpr int kIW = kIT / 64;
 constexpr int kWPT = 8;               // walkers per thread
-constexpr int kWalkers = 256 * kWPT;  // per block
+constexpr int kWalkers = kIT * kWPT;  // per block
+constexpr uint16_t kEnd = 0xffff;
+static_assert(kWalkers <= 0xffff, "walker ids fit 16 bits");
 
-__device__ __forceinline__ void ibwt_one(uint32_t bi, const uint8_t* __restrict__ bwt, size_t stride,
+struct IbwtLds {
+    uint32_t base[kIW][256];   // per-wave byte counts -> merged-vector bases
+    uint32_t seglen[kWalkers];
+    uint32_t sfx[kWalkers];    // suffix sums of segment lengths along the chain
+    uint16_t nxt[kWalkers];    // successor segment (pointer jumping), kEnd past the last
+    uint32_t tmp[kIW];
+    uint32_t period;
+};
+
+__device__ __forceinline__ void ibwt_one(IbwtLds& L, uint32_t bi, const uint8_t* __restrict__ bwt, size_t stride,
                                          const DecBlockInfo* __restrict__ infos, const uint32_t* __restrict__ blocks,
                                          uint32_t* __restrict__ merged, size_t mstride, uint32_t* __restrict__ marks,
                                          size_t kstride, uint8_t* __restrict__ rle1, size_t rstride,
                                          uint32_t* __restrict__ bad_out) {
-    __shared__ uint32_t base[4][256];
-    __shared__ uint32_t seglen[kWalkers];
-    __shared__ uint16_t succ[kWalkers];
-    __shared__ uint32_t segoff[kWalkers];
-    __shared__ uint32_t tmp[8];
     const uint32_t k = blocks[bi];  // decoded-candidate index
     const int t = threadIdx.x, w = wave_id(), lane = lane_id();
     const uint32_t n = infos[k].len;
@@ -707,29 +738,34 @@ __device__ __forceinline__ void ibwt_one(uint32_t bi, const uint8_t* __restrict_
     uint32_t* mark = marks + (size_t)bi * kstride;  // walker id of each start row
     uint8_t* out = rle1 + (size_t)bi * rstride;
     uint32_t* bad = bad_out + bi;
-    // per-wave counts of each byte over the wave's quarter of the block
-    const uint32_t q0 = (uint32_t)((uint64_t)n * w / 4), q1 = (uint32_t)((uint64_t)n * (w + 1) / 4);
-    for (int j = 0; j < 4; ++j) base[w][lane * 4 + j] = 0;
+    // per-wave counts of each byte over the wave's 16th of the block
+    const uint32_t q0 = (uint32_t)((uint64_t)n * w / kIW), q1 = (uint32_t)((uint64_t)n * (w + 1) / kIW);
+    for (int j = 0; j < 4; ++j) L.base[w][lane * 4 + j] = 0;
     __syncthreads();
     for (uint32_t p0 = q0; p0 < q1; p0 += 64) {
         const uint32_t p = p0 + lane;
         const bool v = p < q1;
         const uint32_t c = v ? B[p] : 0u;
         const uint64_t peers = wave_match8(c, v);
-        if (v && (peers & __lanemask_lt()) == 0) atomicAdd(&base[w][c], (uint32_t)__popcll(peers));
+        if (v && (peers & __lanemask_lt()) == 0) atomicAdd(&L.base[w][c], (uint32_t)__popcll(peers));
     }
     __syncthreads();
     {
-        // thread t: byte t -> C[t] + counts of the earlier quarters
-        const uint32_t h = base[0][t] + base[1][t] + base[2][t] + base[3][t];
+        // thread t < 256: byte t -> C[t] + counts of the earlier waves' parts
+        uint32_t h = 0;
+        if (t < 256)
+            for (int q = 0; q < kIW; ++q) h += L.base[q][t];
         uint32_t total;
-        const uint32_t cb = wg_excl_sum<256>(h, tmp, &total);
-        const uint32_t c0 = base[0][t], c1 = base[1][t], c2 = base[2][t];
+        const uint32_t cb = wg_excl_sum<kIT>(h, L.tmp, &total);
         __syncthreads();
-        base[0][t] = cb;
-        base[1][t] = cb + c0;
-        base[2][t] = cb + c0 + c1;
-        base[3][t] = cb + c0 + c1 + c2;
+        if (t < 256) {
+            uint32_t acc = cb;
+            for (int q = 0; q < kIW; ++q) {
+                const uint32_t c = L.base[q][t];
+                L.base[q][t] = acc;
+                acc += c;
+            }
+        }
     }
     __syncthreads();
     for (uint32_t p0 = q0; p0 < q1; p0 += 64) {
@@ -738,9 +774,9 @@ __device__ __forceinline__ void ibwt_one(uint32_t bi, const uint8_t* __restrict_
         const uint32_t c = v ? B[p] : 0u;
         const uint64_t peers = wave_match8(c, v);
         const uint64_t below = peers & __lanemask_lt();
-        const uint32_t r = v ? base[w][c] + (uint32_t)__popcll(below) : 0u;
+        const uint32_t r = v ? L.base[w][c] + (uint32_t)__popcll(below) : 0u;
         __builtin_amdgcn_wave_barrier();
-        if (v && below == 0) base[w][c] += (uint32_t)__popcll(peers);
+        if (v && below == 0) L.base[w][c] += (uint32_t)__popcll(peers);
         __builtin_amdgcn_wave_barrier();
         if (v) M[r] = (p << 8) | c;
     }
@@ -751,16 +787,16 @@ __device__ __forceinline__ void ibwt_one(uint32_t bi, const uint8_t* __restrict_
     __syncthreads();
     auto start_of = [&](int j) -> uint32_t { return j == 0 ? orig : (uint32_t)((uint64_t)n * j / kWalkers); };
     auto is_start = [&](int j) -> bool {
-        const uint32_t s = start_of(j);
-        return n > 0 && (j == 0 || (s != orig && s != start_of(j - 1)));
+        const uint32_t s0 = start_of(j);
+        return n > 0 && (j == 0 || (s0 != orig && s0 != start_of(j - 1)));
     };
-    for (int j = t; j < kWalkers; j += 256) {
-        segoff[j] = 0xffffffffu;
-        seglen[j] = 0;
+    for (int j = t; j < kWalkers; j += kIT) {
+        L.seglen[j] = 0;
+        L.nxt[j] = kEnd;
         if (is_start(j)) {
-            const uint32_t s = start_of(j);
-            mark[s] = (uint32_t)j;
-            M[s] |= 0x80000000u;
+            const uint32_t s0 = start_of(j);
+            mark[s0] = (uint32_t)j;
+            M[s0] |= 0x80000000u;
         }
     }
     __threadfence_block();
@@ -772,7 +808,7 @@ __device__ __forceinline__ void ibwt_one(uint32_t bi, const uint8_t* __restrict_
     bool act[kWPT];
 #pragma unroll
     for (int q = 0; q < kWPT; ++q) {
-        const int j = t + 256 * q;
+        const int j = t + kIT * q;
         act[q] = is_start(j);
         x[q] = start_of(j);
         len[q] = 0;
@@ -800,40 +836,61 @@ __device__ __forceinline__ void ibwt_one(uint32_t bi, const uint8_t* __restrict_
             m[q] = mv[q];
             if (m[q] >> 31) {
                 act[q] = false;
-                seglen[t + 256 * q] = len[q];
-                succ[t + 256 * q] = (uint16_t)mark[x[q]];
+                L.seglen[t + kIT * q] = len[q];
+                const uint32_t sj = mark[x[q]];
+                // the segment that returns to walker 0 ends the chain
+                L.nxt[t + kIT * q] = sj == 0 ? kEnd : (uint16_t)sj;
             } else {
                 any = true;
             }
         }
     }
     __syncthreads();
-    // chain the segments of origPtr's cycle.  A periodic block (T = u^k, the
-    // SURVEY H2 case) has k cycles of n/k rows: the output is the first
-    // cycle's bytes repeated, as the reference's n-step walk produces.
-    __shared__ uint32_t period;
-    if (t == 0) {
-        uint32_t o = 0, j = 0;
-        for (uint32_t guard = 0; guard < (uint32_t)kWalkers && o < n; ++guard) {
-            if (j >= (uint32_t)kWalkers || segoff[j] != 0xffffffffu) break;  // back at walker 0
-            segoff[j] = o;
-            o += seglen[j];
-            j = succ[j];
+    // chain the segments of origPtr's cycle by pointer jumping: sfx[j] = the
+    // lengths from segment j to the chain's last; a segment's offset is
+    // period - sfx[j].  Segments on other cycles never reach kEnd: a periodic
+    // block (T = u^k, the SURVEY H2 case) has k cycles of n/k rows and its
+    // output is the first cycle's bytes repeated, as the reference's n-step
+    // walk produces.
+#pragma unroll
+    for (int q = 0; q < kWPT; ++q) L.sfx[t + kIT * q] = L.seglen[t + kIT * q];
+    __syncthreads();
+    for (int round = 0; (1 << round) < kWalkers; ++round) {
+        uint32_t sv[kWPT];
+        uint16_t nv[kWPT];
+#pragma unroll
+        for (int q = 0; q < kWPT; ++q) {
+            const int j = t + kIT * q;
+            const uint16_t nj = L.nxt[j];
+            sv[q] = L.sfx[j] + (nj != kEnd ? L.sfx[nj] : 0u);
+            nv[q] = nj != kEnd ? L.nxt[nj] : kEnd;
         }
-        period = o;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kWPT; ++q) {
+            L.sfx[t + kIT * q] = sv[q];
+            L.nxt[t + kIT * q] = nv[q];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const uint32_t o = n > 0 && L.nxt[0] == kEnd ? L.sfx[0] : 0u;
+        L.period = o;
         if ((o == 0 || o > n || n % o != 0) && bad) *bad = 1u;
     }
     __syncthreads();
+    const uint32_t per = L.period;
     // pass B: write the bytes of each segment
     uint32_t o[kWPT];
 #pragma unroll
     for (int q = 0; q < kWPT; ++q) {
-        const int j = t + 256 * q;
+        const int j = t + kIT * q;
         act[q] = is_start(j);
         x[q] = start_of(j);
-        const bool placed = act[q] && segoff[j] != 0xffffffffu && segoff[j] + seglen[j] <= period;
-        len[q] = placed ? seglen[j] : 0u;
-        o[q] = placed ? segoff[j] : 0u;
+        const uint32_t sl = L.seglen[j], sf = L.sfx[j];
+        const bool placed = act[q] && L.nxt[j] == kEnd && sf <= per && sl > 0;
+        len[q] = placed ? sl : 0u;
+        o[q] = placed ? per - sf : 0u;
     }
     any = true;
     while (any) {
@@ -851,27 +908,29 @@ __device__ __forceinline__ void ibwt_one(uint32_t bi, const uint8_t* __restrict_
             if (--len[q]) any = true;
         }
     }
-    const uint32_t per = period;
     if (per && per < n && n % per == 0) {
         __threadfence_block();
         __syncthreads();
-        for (uint32_t i = per + t; i < n; i += 256) out[i] = out[i % per];
+        for (uint32_t i = per + t; i < n; i += kIT) out[i] = out[i % per];
     }
 }
 
-// The grid is kept small (a few workgroups per CU, blocks taken in turn) so
-// that the merged vectors being walked at once stay in the 256 MB Infinity
-// Cache: the walks are random 4-byte loads, which from HBM would move a whole
-// line each.
-__global__ __launch_bounds__(256) void dec_ibwt_kernel(const uint8_t* __restrict__ bwt, size_t stride,
+// A persistent grid of one 1024-thread workgroup per CU (BZ2MI_IBWT_XCD
+// per XCD, blocks taken in turn): 8192 walkers per block, 2M loads in flight
+// chip-wide.  The walks are dependent random 4-byte loads, latency-bound:
+// fewer workgroups (to keep the merged vectors in the XCDs' L2) measured
+// slower, 8/16/24/32 per XCD: 101/64/55/58 ms per GiB random (the round-1
+// kernel with 2048 walkers per block and 512 blocks in flight: 62).
+__global__ __launch_bounds__(kIT) void dec_ibwt_kernel(const uint8_t* __restrict__ bwt, size_t stride,
                                                        const DecBlockInfo* __restrict__ infos,
                                                        const uint32_t* __restrict__ blocks, uint32_t nblocks,
                                                        uint32_t* __restrict__ merged, size_t mstride,
                                                        uint32_t* __restrict__ marks, size_t kstride,
                                                        uint8_t* __restrict__ rle1, size_t rstride,
                                                        uint32_t* __restrict__ bad_out) {
+    __shared__ IbwtLds L;
     for (uint32_t bi = blockIdx.x; bi < nblocks; bi += gridDim.x) {
-        ibwt_one(bi, bwt, stride, infos, blocks, merged, mstride, marks, kstride, rle1, rstride, bad_out);
+        ibwt_one(L, bi, bwt, stride, infos, blocks, merged, mstride, marks, kstride, rle1, rstride, bad_out);
         __syncthreads();
     }
 }

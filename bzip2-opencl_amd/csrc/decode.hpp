@@ -54,6 +54,7 @@ __global__ void dec_huff_kernel(const uint8_t* in, uint64_t n, const DecCand* ca
 #define BZ2MI_SYM_BLOCKS 2
 #endif
 constexpr int kDecSymBlocks = BZ2MI_SYM_BLOCKS;  // blocks per wave of dec_sym_kernel
+constexpr int kDecIbwtThreads = 1024;             // threads per dec_ibwt_kernel workgroup
 __global__ void dec_sym_kernel(const uint8_t* in, uint64_t n, const uint8_t* tabs, uint32_t nids, uint32_t smax,
                                uint16_t* syms, size_t sym_stride, DecBlockInfo* infos);
 __global__ void dec_mtf_kernel(const uint16_t* syms, size_t sym_stride, const uint8_t* symmaps,

@@ -55,8 +55,9 @@ struct FrontBufs {
     uint64_t* d_bnd = nullptr;
     uint64_t* d_starts = nullptr;
     uint64_t* d_nb = nullptr;  // [0] blocks, [1] chain status, [2] exit token
+    uint64_t* d_agg = nullptr;  // scan tile aggregates
     std::vector<void*> ptrs() const {
-        return {d_cost, d_dmap, d_summ, d_rsb, d_ccost, d_fc, d_bnd, d_starts, d_nb};
+        return {d_cost, d_dmap, d_summ, d_rsb, d_ccost, d_fc, d_bnd, d_starts, d_nb, d_agg};
     }
 };
 

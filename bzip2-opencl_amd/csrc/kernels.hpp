@@ -124,11 +124,12 @@ __global__ void assemble_kernel(const uint32_t* payload, size_t payload_words, c
 // Device RLE1 front end (frontend.hip); chunks are 4096 bytes.
 constexpr int kFeChunk = 4096;
 __global__ void fe_summary_kernel(const uint8_t* x, uint64_t n, uint64_t nc, uint4* summ);
-constexpr int kFeScanThreads = 1024;  // one workgroup
-__global__ void fe_runscan_kernel(const uint4* summ, uint64_t nc, uint64_t* rsb);
+constexpr int kFeScanThreads = 1024;  // threads per scan workgroup
+constexpr int kFeScanTile = kFeScanThreads * 8;  // chunks per scan workgroup
+__global__ void fe_runscan_kernel(const uint4* summ, uint64_t nc, uint64_t* rsb, uint64_t* agg, int pass);
 __global__ void fe_cost_kernel(const uint8_t* x, uint64_t n, uint64_t nc, const uint4* summ, const uint64_t* rsb,
                                uint8_t* cost, uint32_t* ccost);
-__global__ void fe_costscan_kernel(const uint32_t* ccost, uint64_t nc, uint64_t* fc);
+__global__ void fe_costscan_kernel(const uint32_t* ccost, uint64_t nc, uint64_t* fc, uint64_t* agg, int pass);
 __global__ void fe_dmap_kernel(const uint8_t* x, const uint8_t* cost, uint64_t n, uint64_t nc, const uint64_t* fc,
                                uint8_t* dmap);
 constexpr int kFeChainThreads = 1024;  // one workgroup
