@@ -67,7 +67,6 @@ struct HufShared {
     uint32_t tbits[kMaxTables];
     int lo[kMaxTables], hi[kMaxTables];
     int last[NW][kMaxTables];
-    int mrg[NW][64];
     uint32_t tmp[NW];
 };
 
@@ -194,7 +193,23 @@ __device__ __forceinline__ WaveList mod_list(const WaveList& a, int len) {
 // lanes) and forms their pairs at once.  The result is the reference's array:
 // A[k] = parent of internal node k (+len when it was the second pick) for
 // k < len-2, A[len-2] = root weight, A[len-1] = largest leaf.
-__device__ void ha_parents(int* A, int* IW, int* M, int len) {
+// 64-bit compare-exchange step of a bitonic half-cleaner at lane distance J:
+// the lower lane of each pair keeps the smaller key
+template <int J>
+__device__ __forceinline__ uint64_t half_clean(uint64_t k) {
+    const uint32_t lo = xor_lanes<J>((uint32_t)k), hi = xor_lanes<J>((uint32_t)(k >> 32));
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    const bool lower = (lane_id() & J) == 0;
+    return lower ? (k < o ? k : o) : (k > o ? k : o);
+}
+
+// lane l gets lane 63 - l
+__device__ __forceinline__ uint32_t lane_reverse(uint32_t v) {
+    constexpr int kRowMirror = 0x140;  // row_mirror: lane 15 - l inside each row of 16
+    return xor_lanes<16>(xor_lanes<32>(dpp_mov<kRowMirror>(v)));
+}
+
+__device__ void ha_parents(int* A, int* IW, int len) {
     const int lane = lane_id();
     constexpr int INF = 0x7fffffff;
     if (lane == 0) IW[0] = A[0] + A[1];
@@ -215,24 +230,31 @@ __device__ void ha_parents(int* A, int* IW, int* M, int len) {
             E = 2;
         }
         const int cL = __popcll(bL), cI = __popcll(bI);
-        // merged ranks: leaves before internal nodes of equal weight
-        int nI = 0, nL = 0;  // internal nodes < lw, leaves <= iw
-#pragma unroll
-        for (int step = 64; step > 0; step >>= 1) {
-            const int pi = nI + step - 1, pl = nL + step - 1;
-            const int vi = __shfl(iw, pi & 63), vl = __shfl(lw, pl & 63);
-            if (pi < cI && vi < lw) nI += step;
-            if (pl < cL && vl <= iw) nL += step;
-        }
-        const int rL = lane + nI, rI = lane + nL;
-        const bool takeL = lane < cL && rL < E, takeI = lane < cI && rI < E;
-        if (takeL) M[rL] = lw;
-        if (takeI) {
-            M[rI] = iw;
-            A[ii] = tail + (rI >> 1) + ((rI & 1) ? len : 0);
-        }
-        const int uL = __popcll(__ballot(takeL)), uI = __popcll(__ballot(takeI));
-        if (lane < (E >> 1)) IW[tail + lane] = M[2 * lane] + M[2 * lane + 1];
+        // merged order of the candidates: keys weight << 8 | internal << 7 |
+        // queue position (leaves before internal nodes of equal weight, each
+        // list in its own order), the leaves ascending in lanes, the internal
+        // nodes reversed behind them -- a bitonic sequence whose 64 smallest
+        // one min step and six half-cleaners (DPP / permlane) put in order
+        const uint64_t kl = lane < cL ? ((uint64_t)(uint32_t)lw << 8) | (uint64_t)lane : ~0ull;
+        const uint64_t ki = lane < cI ? ((uint64_t)(uint32_t)iw << 8) | 0x80u | (uint64_t)lane : ~0ull;
+        const uint64_t kr = ((uint64_t)lane_reverse((uint32_t)(ki >> 32)) << 32) | lane_reverse((uint32_t)ki);
+        uint64_t k = kl < kr ? kl : kr;
+        k = half_clean<32>(k);
+        k = half_clean<16>(k);
+        k = half_clean<8>(k);
+        k = half_clean<4>(k);
+        k = half_clean<2>(k);
+        k = half_clean<1>(k);
+        // lane p holds merged position p; positions < E are picked, pairs
+        // (2q, 2q+1) form internal node tail + q
+        const bool take = lane < E;
+        const bool isI = (k >> 7) & 1u;
+        const int w = (int)(uint32_t)(k >> 8);
+        if (take && isI) A[head + (int)(k & 63u)] = tail + (lane >> 1) + ((lane & 1) ? len : 0);
+        const int uI = __popcll(__ballot(take && isI));
+        const int uL = (E - uI);
+        const int wn = (int)xor_lanes<1>((uint32_t)w);
+        if (take && (lane & 1) == 0) IW[tail + (lane >> 1)] = w + wn;
         top += uL;
         head += uI;
         tail += E >> 1;
@@ -317,7 +339,7 @@ __device__ __forceinline__ void wave_bitonic32(uint32_t (&key)[8]) {
             } else {
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-                    const uint32_t o = __shfl_xor(key[e], j);
+                    const uint32_t o = xor_lanes_rt(key[e], j);  // DPP / permlane (j folds to a constant)
                     const bool asc = ((e * 64 + lane) & k) == 0;
                     const bool lower = (lane & j) == 0;
                     key[e] = (lower == asc) ? min(key[e], o) : max(key[e], o);
@@ -350,7 +372,7 @@ __device__ void build_table(HufShared& sh, int q, int alpha, bool stamp = false)
         if (e * 64 + lane < alpha) A[e * 64 + lane] = (int)(key[e] >> 9);
     WaveList a;
     if (alpha > 2) {
-        ha_parents(A, tf, sh.mrg[wave_id()], alpha);  // (tf[q] is free: keys are in registers)
+        ha_parents(A, tf, alpha);  // (tf[q] is free: keys are in registers)
         BZ2MI_PHASE(g_huf_phase, 14, stamp);
         a.load(A, alpha);
         ha_depths(a, alpha);
@@ -446,10 +468,10 @@ int huffman_phases(unsigned long long* out) {
 #endif
 }
 
-// 6 workgroups per CU: the length builds are serial, latency-bound wave code,
+// 7 workgroups per CU (22.6 KB of LDS each): the length builds are serial, latency-bound wave code,
 // so more resident blocks pay for a few spilled registers
 #ifndef BZ2MI_HUF_WGS
-#define BZ2MI_HUF_WGS 6
+#define BZ2MI_HUF_WGS 7
 #endif
 int huffman_threads() { return NT; }
 

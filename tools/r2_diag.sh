@@ -15,6 +15,7 @@ for v in tree $(ls $R/build_v 2>/dev/null | grep -v phases | grep "${VGREP:-.}")
   lib=$R/build_v/$v/libbz2mi.so
   [ $v = tree ] && lib=$R/bzip2-opencl_amd/bz2mi/libbz2mi.so
   for d in ${DATASETS:-random text}; do
+    [ "$d" = none ] && continue
     BZ2MI_LIBRARY=$lib timeout -k 10 200 python3 $R/bench.py --data $d --no-cpu --no-verify > $O/${v}_$d.json 2> $O/${v}_$d.err || { echo "BENCH $v $d FAILED"; tail -5 $O/${v}_$d.err; exit 1; }
     python3 -c "
 import json; d = json.load(open('$O/${v}_$d.json')); print('$v', '$d', d['value'], d['roofline']['stage_ms'])"
