@@ -225,8 +225,8 @@ int stage_mtf(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
 
 int stage_seed(bz2mi_ctx* c, Batch& t, int nb, uint64_t first_block, uint32_t* state, hipStream_t s) {
     using namespace bz2mi;
-    const int ne = c->p * kMaxAlpha;
-    hipLaunchKernelGGL(seed_kernel, dim3((ne + 255) / 256), dim3(256), 0, s, t.d_hist, t.d_seed, state, nb, c->p,
+    const int ng = c->p * ((kMaxAlpha + 63) / 64);
+    hipLaunchKernelGGL(seed_kernel, dim3(ng), dim3(kSeedWaves * 64), 0, s, t.d_hist, t.d_seed, state, nb, c->p,
                        first_block);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("seed");

@@ -81,6 +81,7 @@ __global__ void mtf_kernel(const uint8_t* bwt, size_t stride, const uint32_t* le
                            uint16_t* mtf_out, size_t mtf_stride, uint32_t* mtf_len, uint32_t* alpha_out,
                            uint32_t* hist_out);
 
+constexpr int kSeedWaves = 16;  // waves per seed_kernel workgroup (pieces of a slot's chain)
 __global__ void seed_kernel(const uint32_t* hist, uint32_t* seed, uint32_t* state, int nblocks, int p,
                             uint64_t first_block);
 
