@@ -895,6 +895,46 @@ __device__ __forceinline__ uint32_t wave_sort_lds_text(const uint8_t* __restrict
     return lds_emit_round<E>(T, n, s, start + b0, m, key, src, dst, bwt, orig, idx);
 }
 
+// The same first round straight from a batch's SA entries held in registers
+// (pre[e] = entry e*64+lane): item g = e*64+lane is keyed from pre[e] and its
+// index parked at idx[g] (contiguous stores), so the batch is not counting-
+// sorted into LDS sub-buckets first and its keys are gathered from the text
+// once.  (Any placement of unsorted items over the slots is a valid input of
+// the bitonic network.)
+template <int ES>
+__device__ __forceinline__ uint32_t wave_sort_pre_text(const uint8_t* __restrict__ T, int n, Scratch& s,
+                                                       uint32_t start, uint32_t m, uint32_t d,
+                                                       uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
+                                                       uint32_t* __restrict__ idx,
+                                                       const uint32_t (&pre)[kSmall / 64]) {
+    const int lane = lane_id();
+    uint64_t key[ES];
+#pragma unroll
+    for (int e = 0; e < ES; ++e) {
+        const uint32_t g = (uint32_t)(e * 64 + lane);
+        if (g < m) {
+            const uint32_t i = pre[e];
+            idx[g] = i;
+            uint32_t p = i + d;
+            if (p >= (uint32_t)n) p %= (uint32_t)n;
+            key[e] = ((load8(T, n, p) >> (64 - 8 * kLdsKeyBytes)) << 9) | g;
+        } else {
+            key[e] = ~0ull;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();  // idx[] written before the reads below
+    uint32_t dummy[ES];
+    wave_bitonic<ES, false>(key, dummy);
+    uint32_t src[ES], dst[ES];
+#pragma unroll
+    for (int e = 0; e < ES; ++e) {
+        const uint32_t r = (uint32_t)(lane * ES + e);
+        src[e] = r < m ? idx[key[e] & 511u] : 0u;
+        dst[e] = r;
+    }
+    return lds_emit_round<ES>(T, n, s, start, m, key, src, dst, bwt, orig, idx);
+}
+
 // the tie rounds after a first round left t items tied (depth d + kLdsKeyBytes)
 __device__ __forceinline__ void lds_ties(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t base, uint32_t t,
                                          uint32_t d, const GroupSink& sink, uint8_t* __restrict__ bwt,
@@ -2024,6 +2064,13 @@ __global__ __launch_bounds__(256, 4) void bwt_small_kernel(const uint8_t* __rest
 // ---- kernel 3' (with kernel 1'): the batches the levels queued, per block
 // (one list per block), sorted by one 1024-thread workgroup per block with
 // the block's text in LDS; blocks with an empty list return at once.
+// bwt_block_small_kernel: batches sorted whole from their SA entries in
+// registers (wave_sort_pre_text) instead of wave_sort_bucket2's sub-buckets
+#ifndef BZ2MI_BWT_PRETEXT
+#define BZ2MI_BWT_PRETEXT 1
+#endif
+constexpr bool kBwtPreText = BZ2MI_BWT_PRETEXT != 0;
+
 struct BlockSmallLds {
     uint4 text[kBwtLdsText / 16];
     Bucket3Lds w[FW];
@@ -2076,7 +2123,20 @@ __global__ __launch_bounds__(FT) void bwt_block_small_kernel(const uint8_t* __re
         const uint64_t en = k + FW < nq ? q[k + FW] : 0ull;
         if (k + FW < nq) load_batch(en, nxt);
         const Seg seg{uniform((uint32_t)(ec >> 22) & 0xfffffu), uniform((uint32_t)(ec >> 13) & 511u) + 1u};
-        wave_sort_bucket2(Tl, n, s, seg, uniform((uint32_t)ec & 0x1fffu), sink, out, orig_out + b, L.w[w], cur);
+        const uint32_t d = uniform((uint32_t)ec & 0x1fffu);
+        if constexpr (kBwtPreText) {
+            // the levels' batches are text-like: one sort of the whole batch
+            uint32_t* idx = L.w[w].idx;
+            uint32_t tt;
+            if (seg.len <= 64) tt = wave_sort_pre_text<1>(Tl, n, s, seg.start, seg.len, d, out, orig_out + b, idx, cur);
+            else if (seg.len <= 128) tt = wave_sort_pre_text<2>(Tl, n, s, seg.start, seg.len, d, out, orig_out + b, idx, cur);
+            else if (seg.len <= 256) tt = wave_sort_pre_text<4>(Tl, n, s, seg.start, seg.len, d, out, orig_out + b, idx, cur);
+            else tt = wave_sort_pre_text<8>(Tl, n, s, seg.start, seg.len, d, out, orig_out + b, idx, cur);
+            tt = uniform(tt);
+            if (tt) lds_ties(Tl, n, s, seg.start, tt, d, sink, out, orig_out + b, idx);
+        } else {
+            wave_sort_bucket2(Tl, n, s, seg, d, sink, out, orig_out + b, L.w[w], cur);
+        }
 #pragma unroll
         for (int e = 0; e < E; ++e) cur[e] = nxt[e];
         ec = en;
