@@ -162,7 +162,7 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         for (int mode = 0; mode < (bwt_safree() ? 2 : 1); ++mode)
             hipLaunchKernelGGL(bwt_block_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
                                t.d_sa, t.d_bwt, t.d_orig, c->d_lq[1], lcount + kBwtShards, lcap, t.d_present,
-                               c->d_tq[0], tc[0], tcap, t.d_redo, mode);
+                               c->d_tq[0], tc[0], tcap, t.d_redo, mode, c->d_sq, c->d_scb, tcap);
     } else {
         hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
                            t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap,

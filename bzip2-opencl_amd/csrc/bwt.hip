@@ -1659,10 +1659,17 @@ struct BucketRef {  // a batch's LDS slice (Bucket3Lds layout by pointer)
     uint32_t* idx;
 };
 
+// Pair path of bwt_block_kernel: up to kPair of a block's largest first-byte
+// buckets (> kSmall rotations) are split by their second byte in the same
+// pass (the level-1 partition, with the text in LDS instead of gathered from
+// HBM by the level kernel).
+constexpr int kPair = 16;
+static_assert(kPair <= FW, "one pair slot per wave");
+
 struct BlockLds {
     uint4 text[kBwtLdsText / 16];
     union {
-        uint32_t stage[FT * 8];
+        uint32_t stage[FT * 8 + kPair * 256];  // the tile stage, then the pair cursors
         Bucket3Lds w[FW];
         struct {
             uint32_t base[FW][257];
@@ -1671,6 +1678,8 @@ struct BlockLds {
     } u;
     BwtShared sh;
     uint32_t th[256], ts[256], tmp[FW];
+    uint32_t pbyte[kPair];   // pair slot -> first byte
+    uint8_t pslot[256];      // first byte -> pair slot (0xff: not a pair bucket)
 };
 
 __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict__ blocks, size_t stride,
@@ -1680,7 +1689,9 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
                                                        uint32_t* __restrict__ lcount, size_t lcap,
                                                        uint32_t* __restrict__ present_out, uint64_t* __restrict__ tl,
                                                        uint32_t* __restrict__ tcount, size_t tcap,
-                                                       uint32_t* __restrict__ redo, int mode) {
+                                                       uint32_t* __restrict__ redo, int mode,
+                                                       uint64_t* __restrict__ squeue, uint32_t* __restrict__ scount,
+                                                       size_t scap) {
     __shared__ BlockLds L;
     BwtShared& sh = L.sh;
     const int b = blockIdx.x;
@@ -1798,7 +1809,73 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
         }
         return;
     }
-    // ---- first-byte scatter, one 8192-rotation tile at a time (8 per thread)
+    // ---- pair path: the kPair largest buckets of > kSmall rotations (ties by
+    // byte) get a histogram of their second bytes; wave w < npair turns pair
+    // slot w's counts into child cursors (counts and starts kept in registers)
+    uint32_t* const pair = L.u.stage + FT * 8;
+    const bool big = t < 256 && c > (uint32_t)kSmall;
+    const int npair = min(__syncthreads_count(big), kPair);
+    uint32_t pcnt[4] = {0, 0, 0, 0}, pst[4] = {0, 0, 0, 0};
+    if (npair) {
+        if (t < 256) {
+            uint32_t rk = 0xffu;
+            if (big) {
+                uint32_t above = 0;
+                for (int u = 0; u < 256; ++u) {
+                    const uint32_t cu = sh.hist[u];
+                    above += (cu > c || (cu == c && u < t)) ? 1u : 0u;
+                }
+                if (above < (uint32_t)npair) {
+                    rk = above;
+                    L.pbyte[above] = (uint32_t)t;
+                }
+            }
+            L.pslot[t] = (uint8_t)rk;
+        }
+        for (int k = t; k < kPair * 256; k += FT) pair[k] = 0;
+        __syncthreads();
+        for (int i0 = t * 8; i0 < n; i0 += FT * 8) {
+            const uint2 wv = reinterpret_cast<const uint2*>(Tl)[i0 >> 3];
+            const uint32_t nx = Tl[i0 + 8 < n ? i0 + 8 : 0];
+            uint32_t bv[9];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) bv[k] = ((k < 4 ? wv.x : wv.y) >> ((k & 3) * 8)) & 255u;
+            bv[8] = nx;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = i0 + k;
+                if (i < n) {
+                    const uint32_t ps = L.pslot[bv[k]];
+                    if (ps != 0xffu) {
+                        const uint32_t b1 = i + 1 < n ? bv[k + 1] : (uint32_t)Tl[0];
+                        atomicAdd(&pair[ps * 256u + b1], 1u);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const int w = wave_id(), lane = lane_id();
+        if (w < npair) {
+            uint32_t tot = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                pcnt[j] = pair[w * 256 + lane * 4 + j];
+                pst[j] = tot;
+                tot += pcnt[j];
+            }
+            const uint32_t b0 = sh.base[L.pbyte[w]] + wave_incl_sum(tot) - tot;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                pst[j] += b0;
+                pair[w * 256 + lane * 4 + j] = pst[j];
+            }
+        }
+        __syncthreads();
+    } else if (t < 256) {
+        L.pslot[t] = 0xffu;
+    }
+    // ---- first-byte scatter, one 8192-rotation tile at a time (8 per thread);
+    // rotations of pair buckets go to their (first, second byte) child
     for (int tile0 = 0; tile0 < n; tile0 += FT * 8) {
         if (t < 256) L.th[t] = 0;
         __syncthreads();
@@ -1820,9 +1897,22 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
         for (int k = 0; k < 8; ++k)
             if (i0 + k < n) L.u.stage[L.ts[bv[k]] + rk[k]] = (uint32_t)(i0 + k) | (bv[k] << 24);
         __syncthreads();
-        for (uint32_t j = t; j < tn; j += FT) {
-            const uint32_t v = L.u.stage[j], b8 = v >> 24;
-            sa[sh.base[b8] + (j - L.ts[b8])] = v & 0xffffffu;
+        if (npair == 0) {
+            for (uint32_t j = t; j < tn; j += FT) {
+                const uint32_t v = L.u.stage[j], b8 = v >> 24;
+                sa[sh.base[b8] + (j - L.ts[b8])] = v & 0xffffffu;
+            }
+        } else {
+            for (uint32_t j = t; j < tn; j += FT) {
+                const uint32_t v = L.u.stage[j], b8 = v >> 24, i = v & 0xffffffu;
+                const uint32_t ps = L.pslot[b8];
+                if (ps == 0xffu) {
+                    sa[sh.base[b8] + (j - L.ts[b8])] = i;
+                } else {
+                    const uint32_t b1 = Tl[i + 1 < (uint32_t)n ? i + 1 : 0u];
+                    sa[atomicAdd(&pair[ps * 256u + b1], 1u)] = i;
+                }
+            }
         }
         __syncthreads();
         if (t < 256) sh.base[t] += L.th[t];
@@ -1842,12 +1932,59 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     }
     const Sharded<BwtItem> lqs{lq, lcount, lcap};
     const uint32_t nbat = pack_children(sh);
-    const bool large = t < 256 && c > (uint32_t)kSmall;
+    const bool large = big && L.pslot[t] == 0xffu;
     uint32_t nl;
     const uint32_t rl = wg_excl_sum<FT>(large ? 1u : 0u, L.tmp, &nl);
     if (t == 0) sh.bcast[1] = nl ? lqs.reserve((uint32_t)b, nl) : 0u;
     __syncthreads();
     if (large) lqs.put((uint32_t)b, sh.bcast[1] + rl, BwtItem{(uint32_t)b, ex, c, 1});
+    if (npair) {
+        // the pair buckets' children, as a level-1 partition leaves them: size
+        // 1 final, runs of small ones batched for bwt_block_small_kernel (the
+        // block's list), larger ones to the level queue at depth 2.  Eight
+        // waves at a time (4 KB of packing scratch each).
+        const Sharded<uint64_t> sq{squeue, scount, scap, 0xffffffffu};
+        const int w = wave_id(), lane = lane_id();
+        for (int r0 = 0; r0 < npair; r0 += 8) {
+            if (w >= r0 && w < r0 + 8 && w < npair) {
+                uint32_t* row = pair + w * 256;
+                uint32_t* scr = L.u.stage + (w - r0) * 1024;  // the tile stage is free now
+#pragma unroll
+                for (int j = 0; j < 4; ++j) row[lane * 4 + j] = pcnt[j];
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t nb2 = pack_children_wave(row, scr, scr + 256, scr + 512, scr + 768);
+                uint32_t nlc = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) nlc += pcnt[j] > (uint32_t)kSmall;
+                const uint32_t lex = wave_incl_sum(nlc) - nlc;
+                const uint32_t ltot = (uint32_t)__builtin_amdgcn_readlane((int)(lex + nlc), 63);
+                uint32_t rs = 0, rlq = 0;
+                if (lane == 0) {
+                    rs = nb2 ? sq.reserve((uint32_t)b, nb2) : 0u;
+                    rlq = ltot ? lqs.reserve((uint32_t)b, ltot) : 0u;
+                }
+                rs = uniform(rs);
+                rlq = uniform(rlq) + lex;
+                // the bucket's start: child 0's start (lane 0, element 0)
+                const uint32_t seg0 = (uint32_t)__builtin_amdgcn_readlane((int)pst[0], 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (pcnt[j] == 1u) {
+                        const uint32_t i = sa[pst[j]];
+                        out[pst[j]] = bwt_byte(Tl, n, i);
+                        if (i == 0) orig_out[b] = pst[j];
+                    } else if (pcnt[j] > (uint32_t)kSmall) {
+                        lqs.put((uint32_t)b, rlq++, BwtItem{(uint32_t)b, pst[j], pcnt[j], 2});
+                    }
+                }
+                for (uint32_t k = lane; k < nb2; k += 64) {
+                    const uint32_t bl = scr[768 + k];
+                    sq.put((uint32_t)b, rs + k, sq_pack((uint32_t)b, seg0 + scr[512 + k], bl & 0x7fffffffu, 1u + (bl >> 31)));
+                }
+            }
+            __syncthreads();
+        }
+    }
     // ---- the small batches, one wave each, keys from the LDS text; the next
     // batch's SA entries are loaded while the current one is sorted
     constexpr int E = kSmall / 64;

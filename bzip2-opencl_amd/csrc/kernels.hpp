@@ -38,7 +38,8 @@ bool bwt_safree();  // the SA-free pass is built in (mode 1 needed)
 __global__ void bwt_block_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                                  uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, BwtItem* lq,
                                  uint32_t* lcount, size_t lcap, uint32_t* present_out, uint64_t* tl,
-                                 uint32_t* tcount, size_t tcap, uint32_t* redo, int mode);
+                                 uint32_t* tcount, size_t tcap, uint32_t* redo, int mode, uint64_t* squeue,
+                                 uint32_t* scount, size_t scap);
 __global__ void bwt_level_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                  uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,
                                  int S, const BwtItem* lin, const uint32_t* lin_count, BwtItem* lout,
