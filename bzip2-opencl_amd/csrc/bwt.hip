@@ -731,7 +731,7 @@ __device__ __forceinline__ uint64_t lds_key(const uint8_t* __restrict__ T, int n
     if constexpr (BL::kKeys) {
         return L.key[pos];
     } else {
-        uint32_t p = (L.idx[pos] & 0xffffffu) + d;
+        uint32_t p = (L.idx[pos] & 0x1ffffu) + d;  // LDS text: n < 2^17 (bits 17+: key bits)
         if (p >= (uint32_t)n) p %= (uint32_t)n;
         return load8(T, n, p);
     }
@@ -876,7 +876,7 @@ __device__ __forceinline__ uint32_t wave_sort_lds_text(const uint8_t* __restrict
     for (int e = 0; e < E; ++e) {
         const uint32_t g = (uint32_t)(lane * E + e);
         if (g < m) {
-            uint32_t p = (idx[g] & 0xffffffu) + d;
+            uint32_t p = (idx[g] & 0x1ffffu) + d;
             if (p >= (uint32_t)n) p %= (uint32_t)n;
             key[e] = ((load8(T, n, p) >> (64 - 8 * kLdsKeyBytes)) << 9) | g;
         } else {
@@ -889,7 +889,7 @@ __device__ __forceinline__ uint32_t wave_sort_lds_text(const uint8_t* __restrict
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t g = (uint32_t)(lane * E + e);
-        src[e] = g < m ? idx[key[e] & 511u] & 0xffffffu : 0u;
+        src[e] = g < m ? idx[key[e] & 511u] & 0x1ffffu : 0u;
         dst[e] = g;
     }
     return lds_emit_round<E>(T, n, s, start + b0, m, key, src, dst, bwt, orig, idx);
@@ -1012,7 +1012,10 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
                 uint32_t p = i + d;
                 if (p >= (uint32_t)n) p %= (uint32_t)n;
                 key[e] = load8(T, n, p);
-                ii[e] = i | ((uint32_t)bwt_byte(T, n, i) << 24);
+                if constexpr (BL::kKeys)
+                    ii[e] = i | ((uint32_t)bwt_byte(T, n, i) << 24);
+                else  // LDS text (n < 2^17): the 15 key bits after byte d ride along
+                    ii[e] = i | (((uint32_t)(key[e] >> 41) & 0x7fffu) << 17);
             }
         }
 #pragma unroll
@@ -1059,16 +1062,45 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
     for (int e = 0; e < E; ++e) {
         const uint32_t p = (uint32_t)(e * 64 + lane);
         const bool inseg = p < seg.len;
-        const uint64_t k = inseg ? lds_key(T, n, L, p, d) : 0ull;
         const uint32_t ii = inseg ? L.idx[p] : 0u;
-        const uint32_t c = (uint32_t)(k >> 56);
+        uint32_t lt = 0, le = 0, eqlt = 0, i, c;
+        uint64_t k = 0;
+        bool slow;
+        if constexpr (BL::kKeys) {
+            k = inseg ? lds_key(T, n, L, p, d) : 0ull;
+            c = (uint32_t)(k >> 56);
+            i = ii & 0xffffffu;
+            slow = true;
+        } else {
+            // members compared on the 15 key bits after byte d first (one LDS
+            // word per member instead of an 8-byte key gathered from the
+            // text); only equal prefixes re-read the full keys
+            i = ii & 0x1ffffu;
+            uint32_t pc = i + d;
+            if (pc >= (uint32_t)n) pc %= (uint32_t)n;
+            c = inseg ? (uint32_t)T[pc] : 0u;
+            slow = false;
+        }
         const uint32_t b0 = L.base[c], m = inseg ? L.base[c + 1] - b0 : 0u;
         const bool mine = inseg && m <= (uint32_t)kSub;
-        const uint32_t i = ii & 0xffffffu;
-        uint32_t lt = 0, le = 0, eqlt = 0;
-        for (uint32_t q = 0; q < (mine ? m : 0u); ++q) {
+        if constexpr (!BL::kKeys) {
+            const uint32_t pk = ii >> 17;
+            bool tie = false;
+            for (uint32_t q = 0; q < (mine ? m : 0u); ++q) {
+                const uint32_t pq = L.idx[b0 + q] >> 17;
+                lt += pq < pk;
+                le += pq <= pk;
+                tie |= (pq == pk) & (b0 + q != p);
+            }
+            if (tie) {  // an equal 15-bit prefix: exact counts from the full keys
+                slow = true;
+                lt = le = 0;
+                k = lds_key(T, n, L, p, d);
+            }
+        }
+        for (uint32_t q = 0; q < (mine && slow ? m : 0u); ++q) {
             const uint64_t kq = lds_key(T, n, L, b0 + q, d);
-            const uint32_t iq = L.idx[b0 + q] & 0xffffffu;
+            const uint32_t iq = L.idx[b0 + q] & (BL::kKeys ? 0xffffffu : 0x1ffffu);
             lt += kq < k;
             le += kq <= k;
             eqlt += (kq == k) & (iq < i);
@@ -1076,7 +1108,10 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
         const uint32_t fin = seg.start + b0 + lt + eqlt;
         if (mine) {
             if (s.sa) s.sa[fin] = i;
-            bwt[fin] = (uint8_t)(ii >> 24);
+            if constexpr (BL::kKeys)
+                bwt[fin] = (uint8_t)(ii >> 24);
+            else
+                bwt[fin] = bwt_byte(T, n, i);
             if (i == 0) *orig = fin;
         }
         sink.push_agg(mine && le - lt >= 2 && eqlt == 0, Seg{seg.start + b0 + lt, le - lt}, d + 8);
