@@ -101,15 +101,29 @@ __device__ __forceinline__ uint64_t load8(const uint8_t* __restrict__ T, int n, 
         const uint32_t a = pos & ~3u;
         const uint32_t* T32 = (const uint32_t*)T;
         const uint32_t w0 = T32[a >> 2], w1 = T32[(a >> 2) + 1], w2 = T32[(a >> 2) + 2];
-        const uint32_t sh = (pos & 3u) * 8u;
-        // little-endian words: bytes pos.. are w0 >> sh, then w1, w2
-        const uint32_t lo32 = sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
-        const uint32_t hi32 = sh ? (w1 >> sh) | (w2 << (32 - sh)) : w1;
+        // little-endian words: bytes pos.. are (w1:w0) >> 8 (pos & 3), then (w2:w1)
+        const uint32_t lo32 = __builtin_amdgcn_alignbyte(w1, w0, pos & 3u);
+        const uint32_t hi32 = __builtin_amdgcn_alignbyte(w2, w1, pos & 3u);
         return ((uint64_t)__builtin_bswap32(lo32) << 32) | __builtin_bswap32(hi32);
     }
     uint64_t k = 0;
     uint32_t j = pos;
     for (int q = 0; q < 8; ++q) {
+        k = (k << 8) | T[j];
+        j = (j + 1 == (uint32_t)n) ? 0 : j + 1;
+    }
+    return k;
+}
+
+// 4 bytes of the rotation starting at `pos` (< n), most significant first
+__device__ __forceinline__ uint32_t load4(const uint8_t* __restrict__ T, int n, uint32_t pos) {
+    if (pos + 4 <= (uint32_t)n) {
+        const uint32_t* T32 = (const uint32_t*)T + (pos >> 2);
+        return __builtin_bswap32(__builtin_amdgcn_alignbyte(T32[1], T32[0], pos & 3u));
+    }
+    uint32_t k = 0;
+    uint32_t j = pos;
+    for (int q = 0; q < 4; ++q) {
         k = (k << 8) | T[j];
         j = (j + 1 == (uint32_t)n) ? 0 : j + 1;
     }
@@ -711,6 +725,16 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
 //     sort of their own;
 // all from LDS.  Tie groups go to the sink with their depth.
 constexpr int kSub = 32;
+// sub-bucket ranks by counting (LDS text): members per load round, and whether
+// every element's state is loaded before the first count
+#ifndef BZ2MI_CNT_UNROLL
+#define BZ2MI_CNT_UNROLL 1
+#endif
+#ifndef BZ2MI_CNT_PREFETCH
+#define BZ2MI_CNT_PREFETCH 1
+#endif
+constexpr int kCntUnroll = BZ2MI_CNT_UNROLL;
+constexpr bool kCntPrefetch = BZ2MI_CNT_PREFETCH != 0;
 
 struct Bucket2Lds {
     static constexpr bool kKeys = true;
@@ -1011,11 +1035,14 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
                 const uint32_t i = pre[e];
                 uint32_t p = i + d;
                 if (p >= (uint32_t)n) p %= (uint32_t)n;
-                key[e] = load8(T, n, p);
-                if constexpr (BL::kKeys)
+                if constexpr (BL::kKeys) {
+                    key[e] = load8(T, n, p);
                     ii[e] = i | ((uint32_t)bwt_byte(T, n, i) << 24);
-                else  // LDS text (n < 2^17): the 15 key bits after byte d ride along
-                    ii[e] = i | (((uint32_t)(key[e] >> 41) & 0x7fffu) << 17);
+                } else {  // LDS text (n < 2^17): byte d and the 15 key bits after it ride along
+                    const uint32_t k4 = load4(T, n, p);
+                    key[e] = (uint64_t)k4 << 32;
+                    ii[e] = i | (((k4 >> 9) & 0x7fffu) << 17);
+                }
             }
         }
 #pragma unroll
@@ -1058,63 +1085,95 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
         return;
     }
     // small sub-buckets: ranks by counting (striped positions p = e*64 + lane)
+    if constexpr (BL::kKeys) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t p = (uint32_t)(e * 64 + lane);
-        const bool inseg = p < seg.len;
-        const uint32_t ii = inseg ? L.idx[p] : 0u;
-        uint32_t lt = 0, le = 0, eqlt = 0, i, c;
-        uint64_t k = 0;
-        bool slow;
-        if constexpr (BL::kKeys) {
-            k = inseg ? lds_key(T, n, L, p, d) : 0ull;
-            c = (uint32_t)(k >> 56);
-            i = ii & 0xffffffu;
-            slow = true;
-        } else {
-            // members compared on the 15 key bits after byte d first (one LDS
-            // word per member instead of an 8-byte key gathered from the
-            // text); only equal prefixes re-read the full keys
-            i = ii & 0x1ffffu;
-            uint32_t pc = i + d;
-            if (pc >= (uint32_t)n) pc %= (uint32_t)n;
-            c = inseg ? (uint32_t)T[pc] : 0u;
-            slow = false;
-        }
-        const uint32_t b0 = L.base[c], m = inseg ? L.base[c + 1] - b0 : 0u;
-        const bool mine = inseg && m <= (uint32_t)kSub;
-        if constexpr (!BL::kKeys) {
-            const uint32_t pk = ii >> 17;
-            bool tie = false;
+        for (int e = 0; e < E; ++e) {
+            const uint32_t p = (uint32_t)(e * 64 + lane);
+            const bool inseg = p < seg.len;
+            const uint32_t ii = inseg ? L.idx[p] : 0u;
+            const uint64_t k = inseg ? lds_key(T, n, L, p, d) : 0ull;
+            const uint32_t c = (uint32_t)(k >> 56);
+            const uint32_t i = ii & 0xffffffu;
+            const uint32_t b0 = L.base[c], m = inseg ? L.base[c + 1] - b0 : 0u;
+            const bool mine = inseg && m <= (uint32_t)kSub;
+            uint32_t lt = 0, le = 0, eqlt = 0;
             for (uint32_t q = 0; q < (mine ? m : 0u); ++q) {
-                const uint32_t pq = L.idx[b0 + q] >> 17;
-                lt += pq < pk;
-                le += pq <= pk;
-                tie |= (pq == pk) & (b0 + q != p);
+                const uint64_t kq = lds_key(T, n, L, b0 + q, d);
+                const uint32_t iq = L.idx[b0 + q] & 0xffffffu;
+                lt += kq < k;
+                le += kq <= k;
+                eqlt += (kq == k) & (iq < i);
+            }
+            const uint32_t fin = seg.start + b0 + lt + eqlt;
+            if (mine) {
+                if (s.sa) s.sa[fin] = i;
+                bwt[fin] = (uint8_t)(ii >> 24);
+                if (i == 0) *orig = fin;
+            }
+            sink.push_agg(mine && le - lt >= 2 && eqlt == 0, Seg{seg.start + b0 + lt, le - lt}, d + 8);
+        }
+    } else {
+        // LDS text: members are compared on the 15 key bits after byte d
+        // packed beside their index (one LDS word per member instead of an
+        // 8-byte key gathered from the text); only equal prefixes re-read the
+        // full keys.  Every element's word, sub-bucket byte and bounds are
+        // loaded first (all in flight), then the members four at a time.
+        auto elem_state = [&](int e, uint32_t& w, uint32_t& bm) {
+            const uint32_t p = (uint32_t)(e * 64 + lane);
+            w = p < seg.len ? L.idx[p] : 0u;
+            uint32_t pc = (w & 0x1ffffu) + d;
+            if (pc >= (uint32_t)n) pc %= (uint32_t)n;
+            const uint32_t c = p < seg.len ? (uint32_t)T[pc] : 0u;
+            const uint32_t b0 = L.base[c], m = L.base[c + 1] - b0;
+            bm = p < seg.len && m <= (uint32_t)kSub ? b0 | (m << 9) : 0u;
+        };
+        uint32_t iw[E], sb[E];  // word; b0 | m << 9 (m = 0: not a small sub-bucket of this segment)
+        if constexpr (kCntPrefetch) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) elem_state(e, iw[e], sb[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if constexpr (!kCntPrefetch) elem_state(e, iw[e], sb[e]);
+            const uint32_t p = (uint32_t)(e * 64 + lane);
+            const uint32_t b0 = sb[e] & 511u, mm = sb[e] >> 9;
+            const bool mine = mm != 0;
+            const uint32_t i = iw[e] & 0x1ffffu, pk = iw[e] >> 17;
+            uint32_t lt = 0, le = 0, eqlt = 0;
+            bool tie = false;
+            for (uint32_t q = 0; q < mm; q += kCntUnroll) {
+                uint32_t pq[kCntUnroll];
+#pragma unroll
+                for (int j = 0; j < kCntUnroll; ++j) pq[j] = L.idx[q + j < mm ? b0 + q + j : b0] >> 17;
+#pragma unroll
+                for (int j = 0; j < kCntUnroll; ++j) {
+                    const bool in = q + j < mm;
+                    lt += in & (pq[j] < pk);
+                    le += in & (pq[j] <= pk);
+                    tie |= in & (pq[j] == pk) & (b0 + q + j != p);
+                }
             }
             if (tie) {  // an equal 15-bit prefix: exact counts from the full keys
-                slow = true;
+                const uint64_t k = lds_key(T, n, L, p, d);
                 lt = le = 0;
-                k = lds_key(T, n, L, p, d);
+                for (uint32_t q = 0; q < mm; ++q) {
+                    const uint64_t kq = lds_key(T, n, L, b0 + q, d);
+                    const uint32_t iq = L.idx[b0 + q] & 0x1ffffu;
+                    lt += kq < k;
+                    le += kq <= k;
+                    eqlt += (kq == k) & (iq < i);
+                }
             }
-        }
-        for (uint32_t q = 0; q < (mine && slow ? m : 0u); ++q) {
-            const uint64_t kq = lds_key(T, n, L, b0 + q, d);
-            const uint32_t iq = L.idx[b0 + q] & (BL::kKeys ? 0xffffffu : 0x1ffffu);
-            lt += kq < k;
-            le += kq <= k;
-            eqlt += (kq == k) & (iq < i);
-        }
-        const uint32_t fin = seg.start + b0 + lt + eqlt;
-        if (mine) {
-            if (s.sa) s.sa[fin] = i;
-            if constexpr (BL::kKeys)
-                bwt[fin] = (uint8_t)(ii >> 24);
-            else
+            const uint32_t fin = seg.start + b0 + lt + eqlt;
+            if (mine) {
+#ifndef BZ2MI_DIAG_NOSA
+                if (s.sa) s.sa[fin] = i;
+#endif
                 bwt[fin] = bwt_byte(T, n, i);
-            if (i == 0) *orig = fin;
+                if (i == 0) *orig = fin;
+            }
+            sink.push_agg(mine && le - lt >= 2 && eqlt == 0, Seg{seg.start + b0 + lt, le - lt}, d + 8);
         }
-        sink.push_agg(mine && le - lt >= 2 && eqlt == 0, Seg{seg.start + b0 + lt, le - lt}, d + 8);
     }
     if (nbig) {
 #pragma unroll
