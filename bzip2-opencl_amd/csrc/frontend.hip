@@ -306,7 +306,7 @@ constexpr int kDmapMax = CH + CH / 4 + 64;  // RLE1 output of one chunk, at most
 __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
                                                       uint64_t n, uint64_t nc, const uint64_t* __restrict__ fc,
                                                       uint8_t* __restrict__ dmap) {
-    __shared__ uint8_t stage[4][kDmapMax];
+    __shared__ uint8_t stage[4][kDmapMax + 64];  // + one sink byte per lane
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
     if (c >= nc) return;
     uint8_t* st = stage[wave_id()];
@@ -353,6 +353,12 @@ __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict_
     // (entries of the last byte or two of the input stay unwritten: no target
     // reaches them)
     const uint64_t lim_i = n >= 2 ? n - 2 : 0;  // bytes i <= n-2 have entries
+    // entry r of byte q's piece: Fg(i+2) - y = ci + kn - r, run-start flag.
+    // The first entry is one unconditional store (to the lane's sink byte when
+    // the byte flushes nothing); pieces of 2+ bytes (run ends) add the rest.
+    const uint64_t span = at <= lim_i ? lim_i - at : 0;
+    const uint32_t lim_q = at <= lim_i ? (uint32_t)(span < 63u ? span : 63u) + 1u : 0u;  // bytes q < lim_q have entries
+    const uint32_t sink = (uint32_t)kDmapMax + (uint32_t)lane;
 #pragma unroll
     for (int q = 0; q < 64; ++q) {
         const uint32_t ci = (kv[q >> 2] >> ((q & 3) * 8)) & 255u;
@@ -360,10 +366,11 @@ __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict_
         const uint32_t vn = (xv[(q + 1) >> 2] >> (((q + 1) & 3) * 8)) & 255u;
         const uint32_t kn = (kv[(q + 1) >> 2] >> (((q + 1) & 3) * 8)) & 255u;
         const uint32_t hi = (vn != vq) ? 16u : 0u;
-        if (ci && at + q <= lim_i) {
+        const bool has = ci != 0 && (uint32_t)q < lim_q;
+        st[has ? fl : sink] = (uint8_t)(((ci + kn) & 15u) | hi);
+        if (has && ci > 1) {
 #pragma unroll
-            for (int r = 0; r < 5; ++r)
-                if (r < (int)ci) st[fl + r] = (uint8_t)(((ci + kn - r) & 15u) | hi);  // Fg(i+2) - y, run-start flag
+            for (uint32_t r = 1; r < 5; ++r) st[r < ci ? fl + r : sink] = (uint8_t)(((ci + kn - r) & 15u) | hi);
         }
         fl += ci;
     }
@@ -537,7 +544,10 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
     // resumes the chase when the chain comes back into the windows.  The
     // offsets of jumped-over steps are replayed in parallel afterwards and
     // the block starts written out by all threads.
-    constexpr int kStepsR = 128, kWin = 256, kJ = 16, kGroups = kStepsR / kJ;
+#ifndef BZ2MI_CHAIN_STEPS
+#define BZ2MI_CHAIN_STEPS 256
+#endif
+    constexpr int kStepsR = BZ2MI_CHAIN_STEPS, kWin = 256, kJ = 16, kGroups = kStepsR / kJ;
     constexpr uint32_t kOut = 0x100, kMidRun = 0x200, kEnd = 0x300;  // kOut | D&15
     constexpr uint16_t kStop = 0xffff, kDirect = 0xffff;
     __shared__ uint16_t trans[kStepsR * kWin];
@@ -923,7 +933,10 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
                                                       uint32_t* __restrict__ lens, uint32_t* __restrict__ crcs,
                                                       const uint32_t* __restrict__ crc_tabs) {
     __shared__ uint4 tin4[2 * kTile / 16 + 4];
-    __shared__ uint8_t tout[kTileOut];
+    // tile output window at +16; byte 15 receives a count that belongs to a
+    // piece begun in an earlier tile; then one sink byte per thread
+    __shared__ alignas(16) uint8_t tbuf[16 + kTileOut + 256];
+    uint8_t* const tout = tbuf + 16;
     __shared__ uint32_t tmp[8];
     __shared__ uint32_t lastv[256];
     __shared__ uint32_t tslice[1024], t4096[1024];
@@ -943,7 +956,13 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
     const uint8_t* tin = reinterpret_cast<const uint8_t*>(tin4);
     uint32_t o_carry = 0;
     uint64_t rs_carry = p0;  // run start in effect before the tile
+    const uint32_t blen = (uint32_t)(p1 - p0);  // a block spans < 2^32 input bytes
     for (uint64_t base = p0; base < p1; base += kTile) {
+        // count bytes default to 0 (a piece of exactly 4 that ends here): the
+        // tile's output window is zeroed, so only literal bytes and the counts
+        // of longer pieces are stored
+        reinterpret_cast<uint4*>(tbuf)[t] = make_uint4(0u, 0u, 0u, 0u);
+        if (t < (16 + kTileOut - 4096 + 15) / 16) reinterpret_cast<uint4*>(tbuf)[256 + t] = make_uint4(0u, 0u, 0u, 0u);
         // stage [abase, abase + 16*nvec) covering base-1 .. base+kTile and the
         // CRC bytes from base - pad on
         const uint64_t lo = base == p0 ? p0 : base - pad;
@@ -1022,37 +1041,35 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         }
         uint32_t etot;
         const uint32_t eoff = wg_excl_sum<256>(e, tmp, &etot);
-        // emit into the LDS copy (o: block-relative output position)
+        // emit into the LDS copy (o: block-relative output position); one
+        // store per byte, branch-free: a literal (u <= 3: the 4th byte of a
+        // piece leaves its count slot, zero unless the piece goes on) or the
+        // count of a longer piece at its slot; otherwise the thread's sink byte
         uint32_t o = o_carry + eoff;
         uint32_t un = u0;
+        const uint32_t rel = (uint32_t)(a - p0);
+        const uint32_t sink = (uint32_t)kTileOut + (uint32_t)t;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const uint64_t i = a + q;
+            const uint32_t r = rel + (uint32_t)q;
             uint32_t u = un;
             un = u == 254u ? 0u : u + 1u;
-            if (i < p1) {
-                const uint32_t pv = q ? v[q - 1] : prev;
-                if (i == p0 || v[q] != pv) {
-                    u = 0;
-                    un = 1;
-                }
-                const uint32_t nx = q < 15 ? v[q + 1] : nextb;
-                const bool last = (i + 1 == p1) || nx != v[q] || u == 254;
-                if (u < 3) {
-                    tout[o - o_carry] = v[q];
-                    o++;
-                } else if (u == 3) {
-                    tout[o - o_carry] = v[q];
-                    if (last) tout[o + 1 - o_carry] = 0;  // else the piece's last byte fills the slot
-                    o += 2;
-                } else if (last) {
-                    if (o - 1 >= o_carry) tout[o - 1 - o_carry] = (uint8_t)(u - 3);
-                    else out[o - 1] = (uint8_t)(u - 3);  // piece begun in an earlier tile
-                }
-            }
+            const bool in = r < blen;
+            const uint32_t pv = q ? v[q - 1] : prev;
+            const bool rs = r == 0 || v[q] != pv;
+            u = rs ? 0u : u;
+            un = rs ? 1u : un;
+            const uint32_t nx = q < 15 ? v[q + 1] : nextb;
+            const bool last = r + 1 == blen || nx != v[q] || u == 254u;
+            const bool lit = u <= 3u;
+            const bool st = in && (lit || last);  // (a count slot before the tile: tout[-1])
+            const uint32_t off = o - o_carry - (lit ? 0u : 1u);
+            tout[st ? off : sink] = (uint8_t)(lit ? v[q] : u - 3);
+            o += in ? (u < 3u ? 1u : (u == 3u ? 2u : 0u)) : 0u;
         }
         __syncthreads();
         for (uint32_t j = t; j < etot; j += 256) out[o_carry + j] = tout[j];
+        if (t == 0 && tout[-1]) out[o_carry - 1] = tout[-1];  // counts are >= 1
         o_carry += etot;
         if (tot) rs_carry = p0 + tot - 1;
         __syncthreads();
