@@ -933,10 +933,7 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
                                                       uint32_t* __restrict__ lens, uint32_t* __restrict__ crcs,
                                                       const uint32_t* __restrict__ crc_tabs) {
     __shared__ uint4 tin4[2 * kTile / 16 + 4];
-    // tile output window at +16; byte 15 receives a count that belongs to a
-    // piece begun in an earlier tile; then one sink byte per thread
-    __shared__ alignas(16) uint8_t tbuf[16 + kTileOut + 256];
-    uint8_t* const tout = tbuf + 16;
+    __shared__ uint8_t tout[kTileOut];
     __shared__ uint32_t tmp[8];
     __shared__ uint32_t lastv[256];
     __shared__ uint32_t tslice[1024], t4096[1024];
@@ -956,13 +953,7 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
     const uint8_t* tin = reinterpret_cast<const uint8_t*>(tin4);
     uint32_t o_carry = 0;
     uint64_t rs_carry = p0;  // run start in effect before the tile
-    const uint32_t blen = (uint32_t)(p1 - p0);  // a block spans < 2^32 input bytes
     for (uint64_t base = p0; base < p1; base += kTile) {
-        // count bytes default to 0 (a piece of exactly 4 that ends here): the
-        // tile's output window is zeroed, so only literal bytes and the counts
-        // of longer pieces are stored
-        reinterpret_cast<uint4*>(tbuf)[t] = make_uint4(0u, 0u, 0u, 0u);
-        if (t < (16 + kTileOut - 4096 + 15) / 16) reinterpret_cast<uint4*>(tbuf)[256 + t] = make_uint4(0u, 0u, 0u, 0u);
         // stage [abase, abase + 16*nvec) covering base-1 .. base+kTile and the
         // CRC bytes from base - pad on
         const uint64_t lo = base == p0 ? p0 : base - pad;
@@ -1041,35 +1032,37 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         }
         uint32_t etot;
         const uint32_t eoff = wg_excl_sum<256>(e, tmp, &etot);
-        // emit into the LDS copy (o: block-relative output position); one
-        // store per byte, branch-free: a literal (u <= 3: the 4th byte of a
-        // piece leaves its count slot, zero unless the piece goes on) or the
-        // count of a longer piece at its slot; otherwise the thread's sink byte
+        // emit into the LDS copy (o: block-relative output position)
         uint32_t o = o_carry + eoff;
         uint32_t un = u0;
-        const uint32_t rel = (uint32_t)(a - p0);
-        const uint32_t sink = (uint32_t)kTileOut + (uint32_t)t;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const uint32_t r = rel + (uint32_t)q;
+            const uint64_t i = a + q;
             uint32_t u = un;
             un = u == 254u ? 0u : u + 1u;
-            const bool in = r < blen;
-            const uint32_t pv = q ? v[q - 1] : prev;
-            const bool rs = r == 0 || v[q] != pv;
-            u = rs ? 0u : u;
-            un = rs ? 1u : un;
-            const uint32_t nx = q < 15 ? v[q + 1] : nextb;
-            const bool last = r + 1 == blen || nx != v[q] || u == 254u;
-            const bool lit = u <= 3u;
-            const bool st = in && (lit || last);  // (a count slot before the tile: tout[-1])
-            const uint32_t off = o - o_carry - (lit ? 0u : 1u);
-            tout[st ? off : sink] = (uint8_t)(lit ? v[q] : u - 3);
-            o += in ? (u < 3u ? 1u : (u == 3u ? 2u : 0u)) : 0u;
+            if (i < p1) {
+                const uint32_t pv = q ? v[q - 1] : prev;
+                if (i == p0 || v[q] != pv) {
+                    u = 0;
+                    un = 1;
+                }
+                const uint32_t nx = q < 15 ? v[q + 1] : nextb;
+                const bool last = (i + 1 == p1) || nx != v[q] || u == 254;
+                if (u < 3) {
+                    tout[o - o_carry] = v[q];
+                    o++;
+                } else if (u == 3) {
+                    tout[o - o_carry] = v[q];
+                    if (last) tout[o + 1 - o_carry] = 0;  // else the piece's last byte fills the slot
+                    o += 2;
+                } else if (last) {
+                    if (o - 1 >= o_carry) tout[o - 1 - o_carry] = (uint8_t)(u - 3);
+                    else out[o - 1] = (uint8_t)(u - 3);  // piece begun in an earlier tile
+                }
+            }
         }
         __syncthreads();
         for (uint32_t j = t; j < etot; j += 256) out[o_carry + j] = tout[j];
-        if (t == 0 && tout[-1]) out[o_carry - 1] = tout[-1];  // counts are >= 1
         o_carry += etot;
         if (tot) rs_carry = p0 + tot - 1;
         __syncthreads();
