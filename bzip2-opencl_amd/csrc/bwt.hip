@@ -1139,18 +1139,24 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
             const uint32_t b0 = sb[e] & 511u, mm = sb[e] >> 9;
             const bool mine = mm != 0;
             const uint32_t i = iw[e] & 0x1ffffu, pk = iw[e] >> 17;
-            uint32_t lt = 0, le = 0, eqlt = 0;
+            // the other members only (the element itself: le += 1); a
+            // singleton sub-bucket takes no trip
+            uint32_t lt = 0, le = mine ? 1u : 0u, eqlt = 0;
             bool tie = false;
-            for (uint32_t q = 0; q < mm; q += kCntUnroll) {
+            const uint32_t self = p - b0, others = mine ? mm - 1u : 0u;
+            for (uint32_t q = 0; q < others; q += kCntUnroll) {
                 uint32_t pq[kCntUnroll];
 #pragma unroll
-                for (int j = 0; j < kCntUnroll; ++j) pq[j] = L.idx[q + j < mm ? b0 + q + j : b0] >> 17;
+                for (int j = 0; j < kCntUnroll; ++j) {
+                    const uint32_t r = q + (uint32_t)j;
+                    pq[j] = L.idx[r < others ? b0 + r + (r >= self ? 1u : 0u) : b0] >> 17;
+                }
 #pragma unroll
                 for (int j = 0; j < kCntUnroll; ++j) {
-                    const bool in = q + j < mm;
+                    const bool in = q + (uint32_t)j < others;
                     lt += in & (pq[j] < pk);
                     le += in & (pq[j] <= pk);
-                    tie |= in & (pq[j] == pk) & (b0 + q + j != p);
+                    tie |= in & (pq[j] == pk);
                 }
             }
             if (tie) {  // an equal 15-bit prefix: exact counts from the full keys
