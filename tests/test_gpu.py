@@ -126,6 +126,27 @@ def test_device_api_and_context_reuse(bz):
     assert s1 == s2 == bz.compress(data.tobytes(), 9, 10)
 
 
+def test_input_written_on_null_stream_without_sync(bz):
+    """compress_device with stream 0 orders itself after the input's writers
+    on the null stream (where torch works by default): the input is still being
+    rewritten by queued kernels when the call is made -- no synchronize and no
+    allocation in between (the non-blocking streams must wait)."""
+    import torch
+    n = 64 << 20
+    rng = np.random.default_rng(0x5EED0042)
+    base = rng.integers(0, 256, n, dtype=np.uint8)
+    ctx = bz.Context(9, 10)
+    cap = bz.compress_bound(n)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    x = torch.from_numpy(base).cuda()
+    torch.cuda.synchronize()
+    for _ in range(21):  # an odd number of passes: x = base ^ 0x5A at the end
+        x.bitwise_xor_(0x5A)
+    m = ctx.compress_device(x.data_ptr(), n, out.data_ptr(), cap)
+    got = out[:m].cpu().numpy().tobytes()
+    assert got == bz.compress((base ^ np.uint8(0x5A)).tobytes(), 9, 10)
+
+
 def test_full_size_random_round_trip(bz, cpuref):
     """BASELINE config C2 at full size: the 1 GiB stream at -9, p = 10 is the C
     restatement's (cpu_ref on the host's cores, pinned to O_ref) byte for
