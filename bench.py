@@ -56,10 +56,10 @@ TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r02_traffic_{data}.json")
 
 def stage_traffic(args, stage):
     """HBM-side bytes per launch of `stage` from the committed rocprofv3 --pmc
-    passes of this same command (tools/round_profile.sh -> tools/traffic.py:
+    passes of this same command (tools/measure.sh -> tools/traffic.py:
     FETCH_SIZE x2 per the gfx950 note of MI355X_MICROARCH.md, + WRITE_SIZE).
     Only for the workloads those passes ran (1 GiB of --data random/text at the
-    default level/p/unit; tools/r2_round.sh)."""
+    default level/p/unit; tools/measure.sh)."""
     if args.mib != 1024 or args.level != 9 or args.parallel != 10 or args.unit != 10000:
         return None, None
     path = TRAFFIC_PROFILE.format(data=args.data)
@@ -194,6 +194,7 @@ def main():
     ap.add_argument("--cpu-sample-mib", type=int, default=96)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-900k", action="store_true", help="skip the 900 KB-mode measurement beside the line")
     ap.add_argument("--mode", choices=["compress", "decompress", "e2e"], default="compress",
                     help="compress = the bench line (BASELINE metric); decompress = configs[4]: device "
                          "decompression of the stream this run compresses (output MB/s); e2e = file -> file "
@@ -201,8 +202,9 @@ def main():
     ap.add_argument("--data", choices=["random", "text", "mixed"], default="random",
                     help="random = C2 (the bench line); text = C3 stand-in (seeded word Markov text, enwik9 is "
                          "not available offline); mixed = C4 (rotating random/text/runs/ACGT segments)")
-    ap.add_argument("--units-per-gpu", type=int, default=4,
-                    help="N > 1: units of the logical stream per rank (interleaved over the ranks)")
+    ap.add_argument("--units-per-gpu", type=int, default=None,
+                    help="units of the logical stream per rank (interleaved over the ranks); N > 1 default 4; "
+                         "given at N = 1, the unit protocol runs on the one device (the base of a 1 -> N curve)")
     ap.add_argument("--gather", choices=["none", "rank0"], default="none",
                     help="N > 1: rank0 = also gather the stream onto rank 0 over RCCL inside the timed step; "
                          "none = the stream ends distributed (each rank holds its units' final bytes), the "
@@ -224,7 +226,9 @@ def main():
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
+    if world > 1 or args.units_per_gpu is not None:
+        if args.units_per_gpu is None:
+            args.units_per_gpu = 4
         return bench_units(args, world)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -259,8 +263,6 @@ def main():
     for _ in range(args.warmup):
         out_len = step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     stage_sum = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -268,19 +270,13 @@ def main():
         for k, v in ctx.timings().items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
     stats = ctx.stats()
 
     # correctness: the stream decodes back to the input (prefix check with the
     # host bzip2 decoder; full-size parity lives in tests/)
     verified = None
-    if not args.no_verify and rank == 0:
+    if not args.no_verify:
         import bz2
         head = out[: min(out_len, 4 << 20)].cpu().numpy().tobytes()
         d = bz2.BZ2Decompressor()
@@ -290,10 +286,6 @@ def main():
         except Exception:
             verified = False
 
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
     steps = args.steps
     ms_step = dt / steps * 1e3
     value = world * n * steps / dt / 1e6
@@ -318,6 +310,42 @@ def main():
             "algorithmic_bytes": int(alg[dom]), "avg_ms": round(avg[dom], 3),
             "pipeline_GBps": round((n + out_len) / (ms_step * 1e-3) / 1e9, 2),
             "stage_ms": {k: round(v, 3) for k, v in avg.items()}}
+    # the metric's literal wording, "900KB blocks": the same input at -9 in the
+    # 900 KB mode (unit 100000, S = 900,000; O_ref900 pins),
+    # timed the same way right after the line's own steps
+    mode900 = None
+    if not args.no_900k and args.unit == 10000 and args.level == 9:
+        ctx9 = bz2mi.Context(args.level, args.parallel, 100000, device=local)
+        ctx9.stats()
+        cap9 = bz2mi.compress_bound(n, args.level, 100000)
+        out9 = torch.empty(cap9, dtype=torch.uint8, device=dev)
+        for _ in range(max(1, args.warmup)):
+            z9 = ctx9.compress_device(x.data_ptr(), n, out9.data_ptr(), cap9)
+        torch.cuda.synchronize()
+        st9 = {}
+        t9 = time.perf_counter()
+        for _ in range(args.steps):
+            z9 = ctx9.compress_device(x.data_ptr(), n, out9.data_ptr(), cap9)
+            for k, v in ctx9.timings().items():
+                st9[k] = st9.get(k, 0.0) + v
+        torch.cuda.synchronize()
+        dt9 = time.perf_counter() - t9
+        ok9 = None
+        if not args.no_verify:
+            import bz2
+            head9 = out9[: min(z9, 4 << 20)].cpu().numpy().tobytes()
+            try:
+                got9 = bz2.BZ2Decompressor().decompress(head9, max_length=2 << 20)
+                ok9 = bool(len(got9) > 0 and got9 == x[: len(got9)].cpu().numpy().tobytes())
+            except Exception:
+                ok9 = False
+        mode900 = {"value": round(n * args.steps / dt9 / 1e6, 2), "unit": "MB/s",
+                   "ms_per_step": round(dt9 / args.steps * 1e3, 3), "block_size": args.level * 100000,
+                   "blocks": ctx9.stats()["blocks"], "output_bytes": int(z9), "decode_check": ok9,
+                   "stage_ms": {k: round(v / args.steps, 3) for k, v in st9.items()},
+                   "what": "the same input and steps at -9 in the 900 KB mode (unit 100000; O_ref900 pins)"}
+        del out9
+        ctx9.close()
     cpu = None if args.no_cpu else cpu_baseline(args.cpu_sample_mib << 20)
     refgpu = None if args.no_cpu else reference_gpu(64 << 20)
     line = {
@@ -327,14 +355,13 @@ def main():
         "config": {"workload": WORKLOADS[args.data].format(mib=args.mib),
                    "level": args.level, "block_size": args.level * args.unit, "parallel_blocks": args.parallel,
                    "input_bytes_per_gpu": n, "output_bytes": int(out_len), "ratio": round(out_len / n, 5),
-                   "blocks": nb, "parallelism": f"dp{world} (independent streams)", "decode_check": verified},
+                   "blocks": nb, "parallelism": "dp1 (one stream, one device call)", "decode_check": verified},
         "roofline": roof,
+        "mode_900k": mode900,
         "cpu_baseline": cpu,
         "reference_on_this_gpu": refgpu,
     }
     print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def unit_bytes(args, g: int, U: int, dev):
@@ -357,27 +384,38 @@ def unit_bytes(args, g: int, U: int, dev):
 def bench_units(args, world: int):
     """N ranks, one logical stream (SURVEY.md section 8(e), config C4's layout):
     world x units-per-gpu units of U = mib/units-per-gpu MiB, unit g on rank
-    g mod world; every unit buffer = its bytes + the tail halo (the first
-    bz2mi_unit_halo bytes of unit g+1).  One step = the whole stream through
-    bz2mi.shard: front scans, chain (token in stream order), seed-sum
-    all-gather, Huffman, bit-offset scan, assembly and boundary settling; with
-    --gather rank0 also the ordered RCCL gather onto rank 0."""
+    g mod world; every unit buffer = its bytes + the tail halo (the bytes of the
+    following units, bz2mi_unit_halo of them or up to the stream end).  One
+    step = the whole stream through bz2mi.shard: front scans, chain (token in
+    stream order), seed-sum all-gather, Huffman, bit-offset scan, assembly and
+    boundary settling; with --gather rank0 also the ordered RCCL gather onto
+    rank 0.  world == 1 (--units-per-gpu at --gpus 1): the same protocol on one
+    device, the base of a 1 -> N curve that times the same code at every N.
+    After the timed steps the whole stream is gathered onto rank 0, decoded on
+    the device and compared with every unit's input."""
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BZ2MI_SHARE_GPU=1: rehearsal of the N-rank protocol with every rank on
-    # cuda:0 (one-GPU box): gloo everywhere, no RCCL gather
+    # cuda:0 (one-GPU box): gloo everywhere, pieces gathered over the host
     share = os.environ.get("BZ2MI_SHARE_GPU") == "1"
     if share:
         local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(local)
-    if share:
-        dist.init_process_group("gloo")
-    else:
-        dist.init_process_group("nccl", device_id=dev)
-    ctl = dist.new_group(backend="gloo")
+    ctl = None
+    if world > 1:
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+        ctl = dist.new_group(backend="gloo")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
     ensure_built()
     import bz2mi
     from bz2mi import shard
@@ -389,13 +427,20 @@ def bench_units(args, world: int):
     H = bz2mi.unit_halo(args.level, args.unit)
     ctx = bz2mi.Context(args.level, args.parallel, args.unit, device=local)
     mine = [g for g in range(total) if owners[g] == rank]
-    bufs, halos, units = {}, {}, {}
+    bufs, halos, ends, units = {}, {}, {}, {}
     for g in mine:
-        own = unit_bytes(args, g, U, dev)
-        h = unit_bytes(args, g + 1, U, dev)[:H] if g + 1 < total else own[:0]
-        bufs[g] = torch.cat([own, h])
-        halos[g] = int(h.numel())
-        del own, h
+        # tail halo: the bytes of the following units until H of them or the stream end
+        parts = [unit_bytes(args, g, U, dev)]
+        got, h = 0, g + 1
+        while got < H and h < total:
+            nxt = unit_bytes(args, h, U, dev)[: H - got]
+            parts.append(nxt)
+            got += int(nxt.numel())
+            h += 1
+        bufs[g] = torch.cat(parts)
+        halos[g] = got
+        ends[g] = got < H  # the halo reaches the end of the stream
+        del parts
         units[g] = shard.DeviceUnit(ctx, dev)
     torch.cuda.synchronize()
     out0 = None
@@ -405,18 +450,18 @@ def bench_units(args, world: int):
 
     def step(gather: bool):
         for g in mine:
-            units[g].begin(bufs[g], U, halos[g], g + 1 == total)
+            units[g].begin(bufs[g], U, halos[g], ends[g])
         lay = shard.compress_units(units, owners, args.parallel, args.level, group=ctl)
         settled = shard.settle(lay, ctl)
         if gather:
             shard.gather_stream_device(lay, settled, out0, args.level, dst=0)
         return lay, settled
 
-    gather_in = args.gather == "rank0"
+    gather_in = args.gather == "rank0" and not share
     for _ in range(args.warmup):
         step(gather_in)
     torch.cuda.synchronize()
-    dist.barrier()
+    barrier()
     stage = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -425,39 +470,61 @@ def bench_units(args, world: int):
             for k, v in units[g].timings().items():
                 stage[k] = stage.get(k, 0.0) + v
     torch.cuda.synchronize()
-    dist.barrier()
+    barrier()
     dt = time.perf_counter() - t0
-    tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if share else dev)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    dt = float(tt.item())
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if share else dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
     # the ordered gather onto rank 0, timed once (outside the steps unless --gather rank0)
     gather_ms = None
     if not share:
         torch.cuda.synchronize()
-        dist.barrier()
+        barrier()
         tg = time.perf_counter()
         shard.gather_stream_device(lay, settled, out0, args.level, dst=0)
         torch.cuda.synchronize()
-        dist.barrier()
+        barrier()
         gather_ms = (time.perf_counter() - tg) * 1e3
+    else:  # shared GPU: the pieces travel to rank 0 over the host
+        for g in list(lay.pieces):
+            t, nb = lay.pieces[g]
+            lay.pieces[g] = t[:nb].cpu().numpy().tobytes()
+        host_stream = shard.gather_stream_host(lay, args.level, group=ctl)
+        if rank == 0:
+            out0 = torch.frombuffer(bytearray(host_stream), dtype=torch.uint8).to(dev)
+    # the whole stream, checked once: decoded on the device, every unit's bytes compared
     verified = None
-    if rank == 0 and not args.no_verify and not share:
-        import bz2
-        head = out0[: min(lay.stream_bytes, 4 << 20)].cpu().numpy().tobytes()
-        d = bz2.BZ2Decompressor()
+    if rank == 0 and not args.no_verify:
+        zlen = lay.stream_bytes
+        y = torch.empty(n * world, dtype=torch.uint8, device=dev)
+        d = bz2mi.Decompressor(args.unit)
         try:
-            got = d.decompress(head, max_length=2 << 20)
-            verified = bool(len(got) > 0 and got == bufs[0][: len(got)].cpu().numpy().tobytes())
+            got = d.decompress_device(out0.data_ptr(), zlen, y.data_ptr(), y.numel())
+            verified = got == n * world and all(
+                torch.equal(y[g * U:(g + 1) * U], unit_bytes(args, g, U, dev)) for g in range(total))
         except Exception:
             verified = False
+        del y
+        d.close()
+    vol = {"rle1_bytes": 0, "mtf_symbols": 0, "payload_bits": 0, "blocks": 0}
+    for g in mine:
+        for k, v in units[g].stats().items():
+            vol[k] += v
     if rank == 0:
         steps = args.steps
         ms_step = dt / steps * 1e3
         tot_in = n * world
         value = tot_in * steps / dt / 1e6
         out_bytes = lay.stream_bytes
-        achieved = (tot_in + out_bytes) / (ms_step * 1e-3) / 1e9
-        peak = HBM_PEAK_GBS * world
+        avg = {k: v / steps for k, v in stage.items()}
+        # rank 0's units: algorithmic bytes of the dominant device stage (as the N = 1 line)
+        alg = {"bwt": 2 * vol["rle1_bytes"] + 4 * vol["blocks"],
+               "mtf": vol["rle1_bytes"] + 2 * vol["mtf_symbols"] + 258 * 4 * vol["blocks"],
+               "huffman": 2 * vol["mtf_symbols"] + vol["payload_bits"] // 8}
+        dom = max((k for k in alg if avg.get(k, 0) > 0), key=lambda k: avg[k])
+        achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9
+        cpu = None if args.no_cpu else cpu_baseline(args.cpu_sample_mib << 20)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
@@ -470,21 +537,25 @@ def bench_units(args, world: int):
                        "input_bytes_per_gpu": n, "output_bytes": int(out_bytes), "ratio": round(out_bytes / tot_in, 5),
                        "blocks": int(sum(lay.nblocks)), "parallelism": f"dp{world} (block shards of one stream)",
                        "gather_in_step": gather_in, "decode_check": verified,
+                       "decode_check_what": "whole stream decoded on rank 0's device, every unit's bytes compared",
                        "shared_gpu_rehearsal": share},
-            "roofline": {"bound": "hbm", "kernel": "pipeline (all stages, SURVEY 8(d): (N_in + N_out) / t)",
-                         "achieved": round(achieved, 2), "peak": peak, "unit": "GB/s",
-                         "frac": round(achieved / peak, 4), "traffic": None,
-                         "stage_ms_rank0": {k: round(v / steps, 3) for k, v in stage.items()}},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_rank0": int(alg[dom]), "avg_ms_rank0": round(avg[dom], 3),
+                         "what": "rank 0's units: the dominant stage's algorithmic bytes / its HIP-event time",
+                         "pipeline_GBps": round((tot_in + out_bytes) / (ms_step * 1e-3) / 1e9, 2),
+                         "stage_ms_rank0": {k: round(v, 3) for k, v in avg.items()}},
             "gather": None if gather_ms is None else {
                 "ms": round(gather_ms, 3), "bytes": int(out_bytes),
                 "what": "ordered RCCL point-to-point gather of the settled stream onto rank 0 (once, after the timed "
                         "steps)" if not gather_in else "inside every step",
                 "value_with_gather": round(tot_in / ((ms_step + (0 if gather_in else gather_ms)) * 1e-3) / 1e6, 2)},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    dist.barrier()
-    dist.destroy_process_group()
+    barrier()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 WORKLOAD_DATA = {"random": "random bytes, unit g seeded 0x5EED0001+g", "text": "word-Markov text, unit g seeded "

@@ -31,10 +31,10 @@ EXPORTS = (
     "bz2mi_last_error", "bz2mi_device_count", "bz2mi_version", "bz2mi_create", "bz2mi_destroy",
     "bz2mi_compress_bound", "bz2mi_compress_rle1", "bz2mi_finish", "bz2mi_compress_blocks",
     "bz2mi_compress", "bz2mi_compress_device", "bz2mi_last_timings", "bz2mi_blocks_done",
-    "bz2mi_last_stats", "bz2mi_dcreate", "bz2mi_ddestroy", "bz2mi_decompress", "bz2mi_decompress_device",
+    "bz2mi_last_stats", "bz2mi_dcreate", "bz2mi_ddestroy", "bz2mi_dset_flags", "bz2mi_decompress", "bz2mi_decompress_device",
     "bz2mi_dlast_timings", "bz2mi_unit_halo", "bz2mi_unit_create", "bz2mi_unit_destroy", "bz2mi_unit_begin",
     "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode", "bz2mi_unit_assemble", "bz2mi_unit_timings",
-    "bz2mi_host_alloc", "bz2mi_host_free", "bz2mi_unit_begin_host", "bz2mi_unit_assemble_host",
+    "bz2mi_unit_stats", "bz2mi_host_alloc", "bz2mi_host_free", "bz2mi_unit_begin_host", "bz2mi_unit_assemble_host",
 )
 
 _lib = None
@@ -82,6 +82,8 @@ def lib() -> ctypes.CDLL:
     L.bz2mi_dcreate.restype = c.c_void_p
     L.bz2mi_dcreate.argtypes = [c.c_int, c.c_int]
     L.bz2mi_ddestroy.argtypes = [c.c_void_p]
+    L.bz2mi_dset_flags.restype = c.c_int
+    L.bz2mi_dset_flags.argtypes = [c.c_void_p, c.c_int]
     L.bz2mi_decompress.restype = c.c_int
     L.bz2mi_decompress.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
                                    c.POINTER(c.c_size_t)]
@@ -100,10 +102,11 @@ def lib() -> ctypes.CDLL:
     L.bz2mi_unit_sums.argtypes = [c.c_void_p, c.c_void_p]
     L.bz2mi_unit_encode.argtypes = [c.c_void_p, c.c_void_p, c.POINTER(c.c_uint64), c.POINTER(c.c_uint32)]
     L.bz2mi_unit_assemble.argtypes = [c.c_void_p, c.c_uint64, c.c_uint32, c.c_int, c.c_void_p, c.c_size_t,
-                                      c.POINTER(c.c_size_t)]
+                                      c.POINTER(c.c_size_t), c.c_void_p]
     L.bz2mi_unit_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
+    L.bz2mi_unit_stats.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
     for name in ("bz2mi_unit_begin", "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode",
-                 "bz2mi_unit_assemble", "bz2mi_unit_timings"):
+                 "bz2mi_unit_assemble", "bz2mi_unit_timings", "bz2mi_unit_stats"):
         getattr(L, name).restype = c.c_int
     # debugging entry points (not in include/bz2mi.h)
     L.bz2mi_debug_selftest.restype = c.c_int
@@ -278,9 +281,13 @@ class Unit:
         _check(lib().bz2mi_unit_encode(self._h, c.ctypes.data, ctypes.byref(bits), ctypes.byref(crc)))
         return bits.value, crc.value
 
-    def assemble(self, bit_offset: int, crc_before: int, flags: int, d_out_ptr: int, cap: int) -> int:
+    def assemble(self, bit_offset: int, crc_before: int, flags: int, d_out_ptr: int, cap: int,
+                 stream: int = 0) -> int:
+        """`stream`: the hipStream_t whose queued work may still use the
+        output buffer (0: the null stream); assembly waits for it."""
         n = ctypes.c_size_t(0)
-        _check(lib().bz2mi_unit_assemble(self._h, bit_offset, crc_before, flags, d_out_ptr, cap, ctypes.byref(n)))
+        _check(lib().bz2mi_unit_assemble(self._h, bit_offset, crc_before, flags, d_out_ptr, cap, ctypes.byref(n),
+                                         ctypes.c_void_p(stream)))
         return n.value
 
     def timings(self):
@@ -288,17 +295,28 @@ class Unit:
         _check(lib().bz2mi_unit_timings(self._h, arr))
         return dict(zip(("front", "chain", "bwt", "mtf", "huffman", "assemble"), list(arr)))
 
+    def stats(self):
+        """Volumes once encoded: RLE1 bytes, MTF/RLE2 symbols, payload bits, blocks."""
+        arr = (ctypes.c_uint64 * 4)()
+        _check(lib().bz2mi_unit_stats(self._h, arr))
+        return dict(zip(("rle1_bytes", "mtf_symbols", "payload_bits", "blocks"), [int(v) for v in arr]))
+
 
 class DecompressError(RuntimeError):
     """Corrupt .bz2 data: the reference's std::runtime_error (its message)."""
 
 
+DEC_CONCATENATED = 1
+
+
 class Decompressor:
     """A bz2mi_dctx: device decoder of .bz2 streams (the reference's
     InputStream / BlockDecompressor / HuffmanStageDecoder, InputStream.hpp:36-159).
-    `unit` 10000 accepts the reference's block sizes, 100000 stock bzip2 files."""
+    `unit` 10000 accepts the reference's block sizes, 100000 stock bzip2 files.
+    `concatenated`: decode every stream of the input (bzip2's behaviour); by
+    default only the first, as the reference's InputStream does."""
 
-    def __init__(self, unit: int = 10000, device: int = 0):
+    def __init__(self, unit: int = 10000, device: int = 0, concatenated: bool = False):
         L = lib()
         h = L.bz2mi_dcreate(unit, device)
         if not h:
@@ -306,6 +324,8 @@ class Decompressor:
             raise (ValueError if "Invalid" in msg else RuntimeError)(msg)
         self._h = h
         self.unit = unit
+        if concatenated:
+            _check(L.bz2mi_dset_flags(h, DEC_CONCATENATED))
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -367,9 +387,10 @@ class Decompressor:
         return dict(zip(("scan", "huffman", "mtf", "ibwt", "rle1", "total"), list(arr)))
 
 
-def decompress(data, unit: int = 10000, device: int = 0) -> bytes:
-    """Whole .bz2 (one or more streams) -> bytes, decoded on the device."""
-    with Decompressor(unit, device) as d:
+def decompress(data, unit: int = 10000, device: int = 0, concatenated: bool = False) -> bytes:
+    """Whole .bz2 -> bytes, decoded on the device (the first stream, or every
+    stream with `concatenated`)."""
+    with Decompressor(unit, device, concatenated) as d:
         return d.decompress(data)
 
 

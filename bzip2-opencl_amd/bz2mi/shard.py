@@ -251,11 +251,17 @@ class DeviceUnit:
         need = (need + 255) // 256 * 256
         if self._out is None or self._out.numel() < need:
             self._out = torch.empty(int(need * 1.25) // 4 * 4 + 256, dtype=torch.uint8, device=self.device)
-        nbytes = self.unit.assemble(bit_offset, crc_before, flags, self._out.data_ptr(), self._out.numel())
+        # the buffer may still be read by work queued on torch's current stream
+        # (a previous step's gather / copies): assembly waits for that stream
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        nbytes = self.unit.assemble(bit_offset, crc_before, flags, self._out.data_ptr(), self._out.numel(), stream)
         return self._out, nbytes
 
     def timings(self):
         return self.unit.timings()
+
+    def stats(self):
+        return self.unit.stats()
 
 
 def settle(lay: Layout, ctl_group=None) -> dict:

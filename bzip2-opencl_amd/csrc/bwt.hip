@@ -1144,11 +1144,7 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
             uint32_t lt = 0, le = mine ? 1u : 0u, eqlt = 0;
             bool tie = false;
             const uint32_t self = p - b0, others = mine ? mm - 1u : 0u;
-#ifdef BZ2MI_DIAG_NOLOOP
-            for (uint32_t q = 0; q < 0u; q += kCntUnroll) {
-#else
             for (uint32_t q = 0; q < others; q += kCntUnroll) {
-#endif
                 uint32_t pq[kCntUnroll];
 #pragma unroll
                 for (int j = 0; j < kCntUnroll; ++j) {
@@ -1175,14 +1171,8 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
                 }
             }
             const uint32_t fin = seg.start + b0 + lt + eqlt;
-#ifdef BZ2MI_DIAG_NOEMIT
-            if (mine && fin == 0xffffffffu) {
-#else
             if (mine) {
-#endif
-#ifndef BZ2MI_DIAG_NOSA
                 if (s.sa) s.sa[fin] = i;
-#endif
                 bwt[fin] = bwt_byte(T, n, i);
                 if (i == 0) *orig = fin;
             }
@@ -1984,11 +1974,7 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     }
     // ---- first-byte scatter, one 8192-rotation tile at a time (8 per thread);
     // rotations of pair buckets go to their (first, second byte) child
-#ifdef BZ2MI_DIAG_NOTILE  // diagnostic builds (timing only, wrong output)
-    for (int tile0 = 0; tile0 < 0; tile0 += FT * 8) {
-#else
     for (int tile0 = 0; tile0 < n; tile0 += FT * 8) {
-#endif
         if (t < 256) L.th[t] = 0;
         __syncthreads();
         const int i0 = tile0 + t * 8;
@@ -2113,9 +2099,6 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
         }
     };
     uint32_t cur[E];
-#ifdef BZ2MI_DIAG_NOBATCH
-    if (nbat < 1000000u) return;
-#endif
     if ((uint32_t)w < nbat) load_batch((uint32_t)w, cur);
     for (uint32_t k = (uint32_t)w; k < nbat; k += FW) {
         uint32_t nxt[E];

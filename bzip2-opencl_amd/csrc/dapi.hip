@@ -53,6 +53,7 @@ int grow(T** p, size_t* cap, size_t count) {
 
 struct bz2mi_dctx {
     int unit = 10000, device = 0, cus = 256;
+    int flags = 0;  // BZ2MI_DEC_CONCATENATED: every stream of the input (bzip2), else the first (reference)
     hipStream_t stream = nullptr;
     uint32_t* d_crctab = nullptr;
     uint32_t* d_cnt = nullptr;
@@ -263,6 +264,9 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
         }
         if (!ended) break;
         byte = (pos + 7) / 8;
+        // the reference's InputStream ends at the first end-of-stream marker
+        // (InputStream.hpp:136-143); bzip2 goes on to the next stream
+        if (!(d->flags & BZ2MI_DEC_CONCATENATED)) break;
     }
     // ---- K2b (MTF / RLE2) over the blocks of the chain; its errors (block
     // size, origPtr) end the chain at the first failing block
@@ -469,6 +473,12 @@ int bz2mi_decompress(bz2mi_dctx* d, const uint8_t* in, size_t n, uint8_t* out, s
     r = run_decode(d, d->d_in, n, d->d_out, cap, out_len, d->stream);
     if (r != BZ2MI_OK) return r;
     if (*out_len) DCHECK(hipMemcpy(out, d->d_out, *out_len, hipMemcpyDeviceToHost));
+    return BZ2MI_OK;
+}
+
+int bz2mi_dset_flags(bz2mi_dctx* d, int flags) {
+    if (!d || (flags & ~BZ2MI_DEC_CONCATENATED)) return bz2mi_set_error(BZ2MI_EINVAL, "invalid decoder flags");
+    d->flags = flags;
     return BZ2MI_OK;
 }
 

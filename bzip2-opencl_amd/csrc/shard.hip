@@ -42,6 +42,7 @@ struct bz2mi_unit {
     uint64_t nb = 0, first_block = 0;
     uint32_t* d_state = nullptr;  // p x 258: this unit's slot sums, then the carried seeds
     bz2mi::StreamDev* d_sd = nullptr;
+    unsigned long long* d_vol = nullptr;  // RLE1 bytes, MTF/RLE2 symbols, payload bits (volume_kernel)
     int stage = 0;                // 1 begun, 2 chained, 3 encoded
     uint64_t bits = 0;
     uint32_t crc = 0;
@@ -81,6 +82,7 @@ bz2mi_unit* bz2mi_unit_create(bz2mi_ctx* c) {
     auto* u = new bz2mi_unit();
     u->c = c;
     bool ok = dalloc(&u->d_state, (size_t)c->p * bz2mi::kMaxAlpha) == BZ2MI_OK && dalloc(&u->d_sd, 1) == BZ2MI_OK &&
+              dalloc(&u->d_vol, 4) == BZ2MI_OK &&
               hipEventCreateWithFlags(&u->ev_in, hipEventDisableTiming) == hipSuccess;
     for (auto& e : u->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
     if (!ok) {
@@ -102,6 +104,7 @@ void bz2mi_unit_destroy(bz2mi_unit* u) {
     if (u->d_out) (void)hipFree(u->d_out);
     if (u->d_state) (void)hipFree(u->d_state);
     if (u->d_sd) (void)hipFree(u->d_sd);
+    if (u->d_vol) (void)hipFree(u->d_vol);
     if (u->ev_in) (void)hipEventDestroy(u->ev_in);
     for (auto& e : u->ev)
         if (e) (void)hipEventDestroy(e);
@@ -217,6 +220,8 @@ int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, ui
     if ((r = stage_seed(c, t, cnt, u->first_block, u->d_state, s))) return r;
     if ((r = stage_huffman(c, t, cnt, s))) return r;
     HIPCHECK(hipEventRecord(u->ev[8], s));
+    HIPCHECK(hipMemsetAsync(u->d_vol, 0, 4 * sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(bz2mi::volume_kernel, dim3(16), dim3(256), 0, s, t.d_lens, t.d_mtflen, t.d_pbits, cnt, u->d_vol);
     // bit count and CRC share (offsets from bit 0, stream CRC from 0)
     HIPCHECK(hipMemsetAsync(u->d_sd, 0, sizeof(bz2mi::StreamDev), s));
     hipLaunchKernelGGL(bz2mi::offsets_dev_kernel, dim3(1), dim3(256), 0, s, t.d_pbits, t.d_crc, cnt, u->d_sd, t.d_offs);
@@ -235,7 +240,7 @@ int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, ui
 }
 
 int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags, void* d_out, size_t cap,
-                        size_t* out_bytes) {
+                        size_t* out_bytes, void* hip_stream) {
     if (!stage_ok(u, 3) || !out_bytes || !d_out) return fail(BZ2MI_ESTATE, "bz2mi_unit_assemble: unit not encoded");
     if (((uintptr_t)d_out & 3) != 0) return fail(BZ2MI_EINVAL, "bz2mi_unit_assemble: output not 4-byte aligned");
     bz2mi_ctx* c = u->c;
@@ -258,6 +263,10 @@ int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before,
     const uint64_t cap_words = cap / 4;
     if (((end + 31) / 32) > cap_words) return fail(BZ2MI_ESPACE, "output buffer too small");
     if (cnt == 0) return fail(BZ2MI_EINVAL, "bz2mi_unit_assemble: the unit has no blocks");
+    // d_out may still be read or written by work queued on the caller's
+    // stream (NULL: the null stream): assembly writes it only after that
+    HIPCHECK(hipEventRecord(u->ev_in, (hipStream_t)hip_stream));
+    HIPCHECK(hipStreamWaitEvent(s, u->ev_in, 0));
     HIPCHECK(hipEventRecord(u->ev[9], s));
     HIPCHECK(hipMemcpyAsync(u->d_sd, &sd, sizeof(sd), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(bz2mi::offsets_dev_kernel, dim3(1), dim3(256), 0, s, t.d_pbits, t.d_crc, cnt, u->d_sd, t.d_offs);
@@ -300,7 +309,7 @@ int bz2mi_unit_begin_host(bz2mi_unit* u, const void* host, size_t n_own, size_t 
 }
 
 int bz2mi_unit_assemble_host(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags, void* host_out,
-                             size_t cap, size_t* out_bytes) {
+                             size_t cap, size_t* out_bytes, void* hip_stream) {
     if (!u || !host_out || !out_bytes) return fail(BZ2MI_EINVAL, "null argument");
     bz2mi_ctx* c = u->c;
     HIPCHECK(hipSetDevice(c->device));
@@ -310,10 +319,22 @@ int bz2mi_unit_assemble_host(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_be
         if ((r = dalloc(&u->d_out, need + need / 8))) return r;
         u->out_cap = need + need / 8;
     }
-    int r = bz2mi_unit_assemble(u, bit_offset, crc_before, flags, u->d_out, u->out_cap, out_bytes);
+    int r = bz2mi_unit_assemble(u, bit_offset, crc_before, flags, u->d_out, u->out_cap, out_bytes, hip_stream);
     if (r) return r;
     if (*out_bytes > cap) return fail(BZ2MI_ESPACE, "output buffer too small");
     HIPCHECK(hipMemcpy(host_out, u->d_out, *out_bytes, hipMemcpyDeviceToHost));
+    return BZ2MI_OK;
+}
+
+int bz2mi_unit_stats(bz2mi_unit* u, uint64_t* out4) {
+    if (!u || !out4) return fail(BZ2MI_EINVAL, "null argument");
+    out4[0] = out4[1] = out4[2] = 0;
+    out4[3] = u->nb;
+    if (u->nb == 0 || u->stage < 3) return BZ2MI_OK;
+    HIPCHECK(hipSetDevice(u->c->device));
+    unsigned long long v[4] = {0, 0, 0, 0};
+    HIPCHECK(hipMemcpy(v, u->d_vol, sizeof(v), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 3; ++i) out4[i] = v[i];
     return BZ2MI_OK;
 }
 

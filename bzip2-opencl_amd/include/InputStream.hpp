@@ -8,9 +8,12 @@
 // decoded at once (Huffman tables, MTF/RLE2, inverse BWT, RLE1 and the block /
 // stream CRCs), then bytes are served from the result.  Errors carry the
 // reference's messages; they surface at the first read() instead of after the
-// bytes of the blocks before the bad one.  Blocks may be as large as the
-// bzip2-standard digit x 100,000 bytes, so stock bzip2 streams and bz2mi's
-// 900 KB mode are read too (the reference stops at digit x 10,000).
+// bytes of the blocks before the bad one.  As in the reference, blocks are
+// limited to digit x 10,000 bytes (Config.hpp:30, BlockDecompressor.hpp:
+// 158-162) and decoding ends at the first end-of-stream marker
+// (InputStream.hpp:136-143).  BZ2MI_BZIP2_COMPAT=1 reads like bzip2 instead:
+// digit x 100,000-byte blocks (stock files, bz2mi's 900 KB mode) and every
+// concatenated stream.
 // BZ2MI_HOST_DECODER=1 selects the host decoder below instead (a block at a
 // time, the reference's structure: Huffman tables -> MTF/RLE2 symbols ->
 // inverse BWT -> RLE1 expansion with the block CRC checked).
@@ -93,7 +96,7 @@ private:
         if (magic != static_cast<uint32_t>(STREAM_START_MARKER_1) || h != static_cast<uint32_t>(STREAM_START_MARKER_2) ||
             digit < 1 || digit > 9)
             throw std::runtime_error("Invalid BZip2 header");
-        maxBlock_ = digit * BLOCKSIZE_BZIP2;
+        maxBlock_ = digit * (bzip2Compat() ? BLOCKSIZE_BZIP2 : BLOCKSIZE_DEFAULT);
         started_ = true;
     }
 
@@ -112,6 +115,12 @@ private:
         return refillHost();
     }
 
+    static bool bzip2Compat()
+    {
+        const char *e = std::getenv("BZ2MI_BZIP2_COMPAT");
+        return e && *e && *e != '0';
+    }
+
     // the whole input decoded on the device
     bool refillDevice()
     {
@@ -120,9 +129,12 @@ private:
         int device = 0;
         if (const char *d = std::getenv("BZ2MI_DEVICE"))
             device = std::atoi(d);
-        bz2mi_dctx *d = bz2mi_dcreate(BLOCKSIZE_BZIP2, device);
+        const bool compat = bzip2Compat();
+        bz2mi_dctx *d = bz2mi_dcreate(compat ? BLOCKSIZE_BZIP2 : BLOCKSIZE_DEFAULT, device);
         if (!d)
             throw std::runtime_error(std::string("bz2mi: ") + bz2mi_last_error());
+        if (compat)
+            bz2mi_dset_flags(d, BZ2MI_DEC_CONCATENATED);
         block_.resize(in.size() * 4 + 65536);
         size_t n = 0;
         int rc = bz2mi_decompress(d, reinterpret_cast<const uint8_t *>(in.data()), in.size(), block_.data(),

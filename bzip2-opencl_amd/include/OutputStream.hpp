@@ -207,7 +207,7 @@ private:
         if (stage_.size() < need)
             stage_.resize(need + need / 8);
         size_t n = 0;
-        check(bz2mi_unit_assemble_host(u, nbits_, 0, 0, stage_.data(), stage_.size(), &n));
+        check(bz2mi_unit_assemble_host(u, nbits_, 0, 0, stage_.data(), stage_.size(), &n, nullptr));
         // the first byte shares its top (nbits_ & 7) bits with the pending byte
         if (n > 0)
         {

@@ -171,9 +171,11 @@ int bz2mi_unit_begin(bz2mi_unit* u, const void* d_buf, size_t n_own, size_t n_ha
 int bz2mi_unit_chain(bz2mi_unit* u, uint64_t entry, uint64_t first_block, uint64_t* exit_entry, uint64_t* nblocks);
 int bz2mi_unit_sums(bz2mi_unit* u, uint32_t* sums);
 int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, uint32_t* crc);
-/* d_out: device memory, 4-byte aligned, >= (bits + 7 + 32 + 80) / 8 + 4 bytes */
+/* d_out: device memory, 4-byte aligned, >= (bits + 7 + 32 + 80) / 8 + 4 bytes;
+ * hip_stream: the stream whose queued work may still use d_out (NULL: the null
+ * stream) -- assembly writes d_out only after it; returns when the bytes are in d_out */
 int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags, void* d_out, size_t cap,
-                        size_t* out_bytes);
+                        size_t* out_bytes, void* hip_stream);
 /* Host-memory forms for C++ hosts without a device allocator (the mirror
  * OutputStream): begin_host copies the bytes into a unit-owned device buffer
  * (asynchronous when `host` is pinned; it must stay unchanged until
@@ -182,10 +184,13 @@ void* bz2mi_host_alloc(size_t bytes); /* pinned host memory, NULL on failure */
 void bz2mi_host_free(void* p);
 int bz2mi_unit_begin_host(bz2mi_unit* u, const void* host, size_t n_own, size_t n_halo, int flags);
 int bz2mi_unit_assemble_host(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before, int flags, void* host_out,
-                             size_t cap, size_t* out_bytes);
+                             size_t cap, size_t* out_bytes, void* hip_stream);
 /* milliseconds of the unit's stages (HIP events): front scan, chain (host wall),
  * RLE1 + CRC + BWT, MTF, Huffman, assembly */
 int bz2mi_unit_timings(bz2mi_unit* u, float* ms6);
+/* volumes of the unit once encoded: [0] RLE1 bytes, [1] MTF/RLE2 symbols,
+ * [2] payload bits, [3] blocks */
+int bz2mi_unit_stats(bz2mi_unit* u, uint64_t* out4);
 
 /* ---- decompression on the device ----------
  * Replaces the reference's InputStream (InputStream.hpp:36-159),
@@ -199,13 +204,17 @@ int bz2mi_unit_timings(bz2mi_unit* u, float* ms6);
  * block in stream order as the reference's byte-at-a-time decoder would.
  *   unit   block-size unit of the digit in "BZh<digit>": 10000 = the
  *          reference's limit (Config.hpp:30), 100000 = stock bzip2 files.
- * Concatenated streams are decoded one after another (bzip2's behaviour; the
- * reference stops after the first).  Bytes after the last stream that do not
- * start a new "BZh" header are ignored.
+ * By default only the first stream is decoded and the bytes after its end
+ * marker are ignored (the reference's InputStream, InputStream.hpp:136-143);
+ * with BZ2MI_DEC_CONCATENATED (bz2mi_dset_flags) concatenated streams are
+ * decoded one after another (bzip2's behaviour), and bytes after the last
+ * stream that do not start a new "BZh" header are ignored.
  */
 typedef struct bz2mi_dctx bz2mi_dctx;
+#define BZ2MI_DEC_CONCATENATED 1
 bz2mi_dctx* bz2mi_dcreate(int unit, int device);
 void bz2mi_ddestroy(bz2mi_dctx* d);
+int bz2mi_dset_flags(bz2mi_dctx* d, int flags);
 
 /* host buffers; on BZ2MI_ESPACE *out_len receives the size needed */
 int bz2mi_decompress(bz2mi_dctx* d, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);

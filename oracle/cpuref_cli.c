@@ -24,17 +24,27 @@ int main(int argc, char** argv) {
     long n = ftell(f);
     fseek(f, 0, SEEK_SET);
     unsigned char* in = malloc(n + 1);
-    if (n && fread(in, 1, n, f) != (size_t)n) return 1;
+    if (n && fread(in, 1, n, f) != (size_t)n) {
+        free(in);
+        fclose(f);
+        return 1;
+    }
     fclose(f);
     size_t cap = cpuref_bound(n, level, unit);
     unsigned char* out = malloc(cap);
     long long r = cpuref_compress(in, n, level, p, unit, out, cap, threads);
+    free(in);
     if (r < 0) {
         fprintf(stderr, "compress failed %lld\n", r);
+        free(out);
         return 1;
     }
     FILE* g = fopen(argv[2], "wb");
-    fwrite(out, 1, r, g);
+    if (!g || fwrite(out, 1, r, g) != (size_t)r) {
+        free(out);
+        return 1;
+    }
     fclose(g);
+    free(out);
     return 0;
 }

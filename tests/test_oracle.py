@@ -146,3 +146,43 @@ def test_system_bzip2_accepts_cpuref(tmp_path, cpuref):
     p.write_bytes(cpuref.compress(data, 9, 10))
     r = subprocess.run(["bzip2", "-t", str(p)], capture_output=True)
     assert r.returncode == 0, r.stderr
+
+
+def _asan_cli() -> str:
+    exe = os.path.join(REPO, "oracle", "_build", "cpuref_cli_asan")
+    subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "asan"], check=True, stdout=subprocess.DEVNULL,
+                   stderr=subprocess.DEVNULL)
+    return exe
+
+
+def test_cpuref_under_asan_ubsan(manifest, tmp_path):
+    """The checker itself under AddressSanitizer + UndefinedBehaviorSanitizer
+    (oracle/Makefile `asan`): every golden fixture at every
+    committed setting, single-threaded and on the pthread pool, and two of the
+    pins' multi-block inputs (seed slots reused, runs across blocks), must
+    reproduce the O_ref bytes with no sanitizer report."""
+    import hashlib
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_pins
+    import json
+    exe = _asan_cli()
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    src, dst = tmp_path / "in.bin", tmp_path / "out.bz2"
+
+    def run(data: bytes, level: int, p: int, unit: int = 10000, threads: int = 1) -> bytes:
+        src.write_bytes(data)
+        r = subprocess.run([exe, str(src), str(dst), "-s", str(level), "-p", str(p), "-u", str(unit),
+                            "-j", str(threads)], capture_output=True, text=True, env=env, timeout=600)
+        assert r.returncode == 0 and "runtime error" not in r.stderr and "ERROR" not in r.stderr, r.stderr[-2000:]
+        return dst.read_bytes()
+
+    for i, (name, level, p, file) in enumerate(_cases(manifest)):
+        assert run(golden_input(name), level, p, threads=1 + (i & 1)) == golden_file(file), file
+    with open(os.path.join(GOLDEN, "pins.json")) as f:
+        pins = json.load(f)
+    want = {(p["input"], p["level"], p["p"], p["unit"]): (p["bytes"], p["sha256"]) for p in pins["pins"]}
+    for key in (("mix2m75", 9, 10, 10000), ("run2m75", 9, 3, 10000)):
+        assert key in want, key
+        got = run(make_pins.make_input(key[0]), key[1], key[2], key[3], threads=2)
+        assert (len(got), hashlib.sha256(got).hexdigest()) == want[key], key

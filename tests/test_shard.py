@@ -121,6 +121,70 @@ def test_gloo_two_ranks_one_stream():
     assert all(p.exitcode == 0 for p in procs)
 
 
+class TensorPieceUnit(CpuRefUnit):
+    """A CPU unit whose assemble() returns its bytes as a (uint8 tensor, nbytes)
+    piece with spare room after them, the shape DeviceUnit gives settle() and
+    gather_stream_device() -- so the point-to-point gather runs on gloo ranks."""
+
+    def assemble(self, bit_offset, crc_before, flags):
+        b = super().assemble(bit_offset, crc_before, flags)
+        t = torch.zeros(len(b) + 64, dtype=torch.uint8)
+        t[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        return t, len(b)
+
+
+def _p2p_worker(rank, world, port, q):
+    """settle() + gather_stream_device() across gloo ranks: every unit's piece
+    goes point-to-point (batch_isend_irecv) to rank 0, OR-merging the shared
+    boundary bytes of units that start mid-byte (OutputStream.hpp:225-239)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data = _stream_case(1_500_000, 0x5EED0505)
+    cuts = _cuts(len(data), 13, 9, 10000)
+    bufs = unit_buffers(data, cuts, bz2mi.unit_halo(1, 10000))
+    owners = shard.interleaved_owners(len(bufs), world)
+    units = {}
+    for g, (buf, n_own, n_halo, ends) in enumerate(bufs):
+        if owners[g] == rank:
+            u = TensorPieceUnit(1, 10, 10000)
+            u.begin(buf, n_own, n_halo, ends)
+            units[g] = u
+    lay = shard.compress_units(units, owners, 10, 1)
+    mid = sum(1 for g in range(len(bufs)) if lay.nblocks[g] and g != lay.first and lay.offsets[g] & 7)
+    settled = shard.settle(lay)
+    out = torch.zeros(lay.stream_bytes + 16, dtype=torch.uint8) if rank == 0 else None
+    got = shard.gather_stream_device(lay, settled, out, 1, dst=0)
+    if rank == 0:
+        q.put((bytes(got.numpy().tobytes()) == CpuRef().compress(data, 1, 10), mid,
+               len({owners[g] for g in range(len(bufs)) if lay.nblocks[g]})))
+    else:
+        assert got is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_p2p_gather_one_stream(world):
+    """The ordered point-to-point gather of bz2mi.shard (the RCCL path of config
+    C4) on CPU tensors over gloo: both sides of batch_isend_irecv, units that
+    start mid-byte, pieces on every rank -> the single-stream cpu_ref bytes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_p2p_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok, mid, ranks = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert ok
+    assert mid >= 3, "the layout must exercise mid-byte unit boundaries"
+    assert ranks == world, "every rank must hold pieces"
+    assert all(p.exitcode == 0 for p in procs)
+
+
 # ---------------------------------------------------------------- device ----
 
 def _device_units(ctx, data_t: torch.Tensor, cuts: list[int], owners, rank, level, unit=10000):

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 measurement set, part A (one gpurun call): all GPU tests, the default
+# Measurement set, part A (one gpurun call): all GPU tests, the default
 # bench line (with CPU baselines), rocprofv3 kernel stats of the default line and
 # FETCH_SIZE / WRITE_SIZE passes (separate --pmc runs, kernel trace only).
 # PART=B instead: the text workload's stats + PMC passes and the secondary lines.

@@ -1,4 +1,4 @@
-"""Per-launch HBM-side traffic of the bz2mi kernels from tools/round_profile.sh's
+"""Per-launch HBM-side traffic of the bz2mi kernels from tools/measure.sh's
 two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; kB per dispatch).
 
 The bench command of those passes runs 2 compressions (1 warmup + 1 step);
@@ -15,7 +15,7 @@ import sys
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/round"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01_traffic.json"
 steps = 2
-suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # e.g. "_random" for tools/r2_round.sh
+suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # e.g. "_random" for tools/measure.sh
 workload = sys.argv[4] if len(sys.argv) > 4 else "C2"
 per = collections.defaultdict(lambda: {"fetch_bytes": 0.0, "write_bytes": 0.0, "dispatches": 0})
 for counter, sub, scale in (("FETCH_SIZE", "pmc_fetch", 2.0), ("WRITE_SIZE", "pmc_write", 1.0)):
