@@ -154,9 +154,13 @@ class Context:
         self._h = h
         self.level, self.parallel, self.unit = level, parallel, unit
         self.block_size = level * unit
+        import weakref
+        self._units = weakref.WeakSet()  # units on this context: closed before it
 
     def close(self) -> None:
         if getattr(self, "_h", None):
+            for u in list(self._units):
+                u.close()
             lib().bz2mi_destroy(self._h)
             self._h = None
 
@@ -246,6 +250,7 @@ class Unit:
         self._h = h
         self.ctx = ctx  # keeps the context alive
         self.parallel = ctx.parallel
+        ctx._units.add(self)
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -216,8 +216,9 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
 
 int stage_mtf(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     using namespace bz2mi;
-    hipLaunchKernelGGL(mtf_kernel, dim3(nb), dim3(64), 0, s, t.d_bwt, c->stride, t.d_lens, nb, t.d_present, t.d_mtf,
-                       c->mtf_stride, t.d_mtflen, t.d_alpha, t.d_hist);
+    // segment scratch: the block's SA area (free after the BWT), stride uint32 = 2 * stride u16
+    launch_mtf(nb, t.d_bwt, c->stride, t.d_lens, t.d_present, t.d_mtf, c->mtf_stride, t.d_mtflen, t.d_alpha, t.d_hist,
+               reinterpret_cast<uint16_t*>(t.d_sa), 2 * c->stride, s);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("mtf");
     return BZ2MI_OK;

@@ -77,10 +77,12 @@ __host__ __device__ inline size_t bwt_lqueue_per_block(int S) { return (size_t)S
 // per-block group list capacity (BwtSeg entries) for a block stride
 __host__ __device__ inline size_t bwt_group_stride(size_t stride) { return stride / 2 + 2; }
 
-// MTF + RLE2, one wave per block; `present` (8 words per block) comes from bwt_bucket_kernel
-__global__ void mtf_kernel(const uint8_t* bwt, size_t stride, const uint32_t* lens, int nblocks, const uint32_t* present,
-                           uint16_t* mtf_out, size_t mtf_stride, uint32_t* mtf_len, uint32_t* alpha_out,
-                           uint32_t* hist_out);
+// MTF + RLE2, one workgroup of 1..8 waves per block (segments when the batch
+// has few blocks; `scratch`: scratch_stride u16 per block, the segments'
+// output before concatenation); `present` (8 words per block) comes from the BWT
+void launch_mtf(int nb, const uint8_t* bwt, size_t stride, const uint32_t* lens, const uint32_t* present,
+                uint16_t* mtf_out, size_t mtf_stride, uint32_t* mtf_len, uint32_t* alpha_out, uint32_t* hist_out,
+                uint16_t* scratch, size_t scratch_stride, hipStream_t s);
 
 constexpr int kSeedWaves = 16;  // waves per seed_kernel workgroup (pieces of a slot's chain)
 __global__ void seed_kernel(const uint32_t* hist, uint32_t* seed, uint32_t* state, int nblocks, int p,

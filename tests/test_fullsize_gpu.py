@@ -88,7 +88,7 @@ def test_c4_8gib_units_equal_single_stream():
     got = shard.gather_stream_device(lay, shard.settle(lay), out, level)
     assert got.numel() == m
     assert torch.equal(got, whole)
-    del units, lay, out, got
+    del units, lay, out, got, u
     ctx.close()
     torch.cuda.empty_cache()
     # and back on the device
