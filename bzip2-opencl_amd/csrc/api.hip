@@ -159,10 +159,25 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     if (blk) {
         HIPCHECK(hipMemsetAsync(c->d_scb, 0, nb * sizeof(uint32_t), s));
         HIPCHECK(hipMemsetAsync(t.d_redo, 0, nb * sizeof(uint32_t), s));
-        for (int mode = 0; mode < (bwt_safree() ? 2 : 1); ++mode)
+        // mode 0 defers text-like blocks to the induced-sorting text kernel,
+        // mode 1 takes the ones it hands back
+        static const bool text_path = [] {
+            const char* e = getenv("BZ2MI_TEXTBWT");
+            return !(e && *e == '0');
+        }();
+        for (int mode = 0; mode < 2; ++mode) {
+            if (mode == 1 && text_path) {
+                hipLaunchKernelGGL(bwt_text_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
+                                   t.d_sa, t.d_bwt, t.d_orig, t.d_present, t.d_redo, c->d_lspill, t.d_groups);
+                HIPCHECK(hipGetLastError());
+            }
+            if (mode == 1 && !text_path) {  // every text-like block back to the general path
+                hipLaunchKernelGGL(redo_all_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, t.d_redo, nb);
+            }
             hipLaunchKernelGGL(bwt_block_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
                                t.d_sa, t.d_bwt, t.d_orig, c->d_lq[1], lcount + kBwtShards, lcap, t.d_present,
                                c->d_tq[0], tc[0], tcap, t.d_redo, mode, c->d_sq, c->d_scb, tcap);
+        }
     } else {
         hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
                            t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap,
@@ -170,6 +185,15 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     }
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");
+    if (blk && getenv("BZ2MI_BWT_STATS")) {  // debug: how the blocks went (0 general, 1 text, 2 handed back)
+        std::vector<uint32_t> r(nb);
+        HIPCHECK(hipMemcpyAsync(r.data(), t.d_redo, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        unsigned cnt[4] = {0, 0, 0, 0};
+        for (uint32_t v : r) cnt[v < 4 ? v : 3]++;
+        fprintf(stderr, "[bz2mi] bwt blocks: general %u, text %u, handed back %u\n", cnt[0], cnt[1], cnt[2] + cnt[3]);
+
+    }
     static const bool wlevel = [] {
         const char* e = getenv("BZ2MI_WLEVEL");
         return !(e && *e == '0');

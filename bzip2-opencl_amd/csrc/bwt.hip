@@ -1738,24 +1738,11 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
 constexpr int FT = 1024;
 constexpr int FW = FT / 64;
 
-// SA-free pass (blocks whose first-byte buckets are all <= kSmall): the
-// rotation indices of a run of batches are staged in LDS (kPassIdx at a time)
-// and sorted in place there; each wave keeps only its sub-bucket bases.  It
-// removes the SA round trips (8.6 GB per GiB of random input) but measured
-// slower -- random BWT 12.5 -> 17.6 ms per GiB: a text scan and two barriers
-// per pass of ~32 batches cost more than the global first-byte scatter they
-// replace -- so it is off (BZ2MI_BWT_SAFREE=1 builds it in, bwt_safree()).
-#ifndef BZ2MI_BWT_SAFREE
-#define BZ2MI_BWT_SAFREE 0
-#endif
-constexpr bool kBwtSaFree = BZ2MI_BWT_SAFREE != 0;
-constexpr int kPassIdx = 11264;
-
-struct BucketRef {  // a batch's LDS slice (Bucket3Lds layout by pointer)
-    static constexpr bool kKeys = false;
-    uint32_t* base;
-    uint32_t* idx;
-};
+// Text-like blocks (at most kTextAlpha distinct bytes) are deferred by mode 0
+// to bwt_text_kernel (redo[b] = 1), which hands back the ones it cannot finish
+// (redo[b] = 2: periodic or very long repeats, a full work queue) to mode 1.
+constexpr int kTextAlpha = 64;    // distinct bytes of a text-path block
+constexpr int kTextMinN = 4096;   // smaller blocks stay on this path
 
 // Pair path of bwt_block_kernel: up to kPair of a block's largest first-byte
 // buckets (> kSmall rotations) are split by their second byte in the same
@@ -1769,10 +1756,6 @@ struct BlockLds {
     union {
         uint32_t stage[FT * 8 + kPair * 256];  // the tile stage, then the pair cursors
         Bucket3Lds w[FW];
-        struct {
-            uint32_t base[FW][257];
-            uint32_t idx[kPassIdx];
-        } pass;
     } u;
     BwtShared sh;
     uint32_t th[256], ts[256], tmp[FW];
@@ -1794,8 +1777,8 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     BwtShared& sh = L.sh;
     const int b = blockIdx.x;
     if (b >= nblocks) return;
-    // mode 1: only the blocks the SA-free pass of mode 0 handed back
-    if (mode == 1 && redo[b] == 0u) return;
+    // mode 1: only the blocks the text kernel handed back
+    if (mode == 1 && redo[b] < 2u) return;
     const int t = threadIdx.x;
     const int n = (int)uniform(lens[b]);
     const uint8_t* T = blocks + (size_t)b * stride;
@@ -1832,80 +1815,20 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     uint32_t total;
     const uint32_t ex = wg_excl_sum<FT>(c, L.tmp, &total);
     if (t < 256) sh.base[t] = ex;
-    if (kBwtSaFree && mode == 0 && !__syncthreads_or(c > (uint32_t)kSmall)) {
-        // ---- SA-free pass: every bucket is small, so the whole BWT is the
-        // batch sorts.  Runs of batches of up to kPassIdx rotations: their
-        // indices are staged in LDS by a scan of the LDS text, sorted in place
-        // by one wave per batch, and only BWT bytes and origPtr leave the
-        // workgroup.  A tie group (equal 8-byte keys) hands the block to mode 1.
-        if (t < 256) {
-            const uint64_t m = __ballot(c != 0);
-            if (lane_id() == 0) {
-                present_out[(size_t)b * 8 + 2 * wave_id()] = (uint32_t)m;
-                present_out[(size_t)b * 8 + 2 * wave_id() + 1] = (uint32_t)(m >> 32);
-            }
-        }
-        const uint32_t nbat = pack_children(sh);
-        // buckets of one rotation are final (batches made only of them are
-        // dropped by pack_children): their BWT byte straight from the text
-        for (int i0 = t * 8; i0 < n; i0 += FT * 8) {
-            const uint2 wv = reinterpret_cast<const uint2*>(Tl)[i0 >> 3];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t v = ((k < 4 ? wv.x : wv.y) >> ((k & 3) * 8)) & 255u;
-                if (i0 + k < n && sh.hist[v] == 1u) {
-                    const uint32_t i = (uint32_t)(i0 + k), pos = sh.base[v];
-                    out[pos] = bwt_byte(Tl, n, i);
-                    if (i == 0) orig_out[b] = pos;
+    if (mode == 0) {
+        // text-like blocks: the symbol map, then bwt_text_kernel
+        const int K = __syncthreads_count(c != 0u);
+        if (K <= kTextAlpha && n >= kTextMinN) {
+            if (t < 256) {
+                const uint64_t m = __ballot(c != 0);
+                if (lane_id() == 0) {
+                    present_out[(size_t)b * 8 + 2 * wave_id()] = (uint32_t)m;
+                    present_out[(size_t)b * 8 + 2 * wave_id() + 1] = (uint32_t)(m >> 32);
                 }
             }
+            if (t == 0) redo[b] = 1u;
+            return;
         }
-        const int w = wave_id(), lane = lane_id();
-        constexpr int E = kSmall / 64;
-        Scratch s{};
-        s.sa = nullptr;
-        GroupSink sink{};
-        sink.redo = redo + b;
-        for (uint32_t k0 = 0; k0 < nbat;) {
-            if (t == 0) {
-                const uint32_t p0 = sh.bat_start[k0];
-                uint32_t k1 = k0 + 1;
-                while (k1 < nbat && sh.bat_start[k1] + (sh.bat_len[k1] & 0x7fffffffu) - p0 <= (uint32_t)kPassIdx) ++k1;
-                sh.bcast[0] = k1;
-                sh.bcast[1] = p0;
-                sh.bcast[2] = sh.bat_start[k1 - 1] + (sh.bat_len[k1 - 1] & 0x7fffffffu);
-            }
-            if (t < 256) L.th[t] = 0;
-            __syncthreads();
-            const uint32_t k1 = sh.bcast[0], pst = sh.bcast[1], pend = sh.bcast[2];
-            // stage the pass's rotation indices by first byte
-            for (int i0 = t * 8; i0 < n; i0 += FT * 8) {
-                const uint2 wv = reinterpret_cast<const uint2*>(Tl)[i0 >> 3];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint32_t v = ((k < 4 ? wv.x : wv.y) >> ((k & 3) * 8)) & 255u;
-                    const uint32_t bs = sh.base[v];
-                    if (i0 + k < n && bs >= pst && bs < pend)
-                        L.u.pass.idx[bs - pst + atomicAdd(&L.th[v], 1u)] = (uint32_t)(i0 + k);
-                }
-            }
-            __syncthreads();
-            for (uint32_t k = k0 + (uint32_t)w; k < k1; k += FW) {
-                const uint32_t bl = uniform(sh.bat_len[k]);
-                const Seg seg{uniform(sh.bat_start[k]), bl & 0x7fffffffu};
-                BucketRef R{L.u.pass.base[w], L.u.pass.idx + (seg.start - pst)};
-                uint32_t pre[E];
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const uint32_t g = (uint32_t)(e * 64 + lane);
-                    pre[e] = g < seg.len ? R.idx[g] : 0u;
-                }
-                wave_sort_bucket2(Tl, n, s, seg, bl >> 31, sink, out, orig_out + b, R, pre);
-            }
-            __syncthreads();
-            k0 = k1;
-        }
-        return;
     }
     // ---- pair path: the kPair largest buckets of > kSmall rotations (ties by
     // byte) get a histogram of their second bytes; wave w < npair turns pair
@@ -2111,7 +2034,6 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     }
 }
 
-bool bwt_safree() { return kBwtSaFree; }
 
 // ---- kernel 2 (one launch per level, all blocks at once): every large
 // segment of the level queue is partitioned by one workgroup.  The last level
@@ -2376,6 +2298,417 @@ __global__ __launch_bounds__(FT) void bwt_block_small_kernel(const uint8_t* __re
         for (int e = 0; e < E; ++e) cur[e] = nxt[e];
         ec = en;
     }
+}
+
+// ---- kernel 1t: text-like blocks (at most kTextAlpha distinct bytes), one
+// 1024-thread workgroup per block with the block's text in LDS.  Induced
+// sorting in the manner of bzip2's main sort (Seward's "copy" step):
+//   * every rotation is scattered into its two-byte bucket (a, b);
+//   * the first-byte buckets are processed in ascending size; for bucket ss
+//     every pair bucket (ss, b) whose b is not yet processed (and (ss, ss)) is
+//     sorted -- partitions by the next byte and wave sorts, all keys read from
+//     the LDS text, work spread over the 16 waves through an LDS work queue --
+//     while the pair buckets (ss, b) of processed b are already in order;
+//   * then bucket ss is complete, and for every unprocessed x the pair bucket
+//     (x, ss) follows for free: the rotations i-1 of the sorted bucket ss with
+//     T[i-1] = x, in that order (a stable partition by the preceding byte).
+// About half of the rotations of text are placed by the copy step without
+// being sorted.  BWT bytes and origPtr are written as positions become final.
+// Blocks it cannot finish (ties deeper than kTextDcap bytes: periodic blocks,
+// very long repeats; a full work queue) get redo[b] = 2 and go through the
+// general path (bwt_block_kernel mode 1).
+constexpr int kTextDcap = 512;   // depth at which a tie or a partition gives up
+
+constexpr int kTQ = 512;         // work items per round
+constexpr int kTW = 768;         // per-wave LDS words
+
+struct TextLds {
+    uint4 text[kBwtLdsText / 16];
+    union {
+        uint32_t cur[kTextAlpha * kTextAlpha];  // pair-bucket cursors (the scatter)
+        uint32_t w[FW][kTW];                    // per-wave scratch (the steps)
+    } u;
+    uint64_t q[2][kTQ];               // work items of this round / the next: depth | len | start
+    uint32_t pcol[kTextAlpha];        // start of (x, ss) for the copy targets
+    uint32_t cstart[kTextAlpha + 1];  // first-byte bucket starts
+    uint32_t tmp[FW];
+    uint32_t qn[2], fail;
+    uint8_t id[256];                  // byte -> dense id
+    uint8_t order[kTextAlpha];        // ids by ascending bucket size
+    uint8_t done[kTextAlpha];
+    uint8_t target[kTextAlpha];
+};
+
+// SA / spill words the text kernel reads back after other waves (or this
+// one) rewrote them within the launch: device-coherent loads that bypass the
+// CU's vector L1, which may still hold the line from an earlier read
+__device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t tq_item(uint32_t start, uint32_t len, uint32_t depth) {
+    return ((uint64_t)(depth & 0xffffu) << 34) | ((uint64_t)len << 17) | (uint64_t)start;  // start, len < 2^17
+}
+
+// append the items of the lanes with `want` to the next round's list
+// (wave-aggregated); a full list means the block gives up
+__device__ __forceinline__ void tq_push(TextLds& L, int nxt, bool want, uint32_t start, uint32_t len,
+                                        uint32_t depth) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&L.qn[nxt], (uint32_t)__popcll(m));
+    base = uniform(base);
+    if (want) {
+        const uint32_t pos = base + (uint32_t)__popcll(m & __lanemask_lt());
+        if (pos < (uint32_t)kTQ) L.q[nxt][pos] = tq_item(start, len, depth);
+        else atomicOr(&L.fail, 1u);
+    }
+}
+
+// match of a 6-bit value over the valid lanes
+__device__ __forceinline__ uint64_t wave_match6(uint32_t key, bool valid) {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+        const bool bit = (key >> b) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+    }
+    return peers;
+}
+
+// a rotation's final position: its BWT byte (and origPtr)
+__device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t pos, uint32_t i, uint8_t* out,
+                                           uint32_t* orig) {
+    out[pos] = bwt_byte(Tl, n, i);
+    if (i == 0) *orig = pos;
+}
+
+// sort a segment of <= kSmall rotations with a common prefix of d bytes (one
+// wave; keys from the LDS text); final SA entries, BWT bytes, origPtr
+__device__ void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out, uint32_t* orig,
+                          uint32_t* W, TextLds& L) {
+    constexpr int E = kSmall / 64;
+    const int lane = lane_id();
+    uint32_t pre[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(e * 64 + lane);
+        pre[e] = g < seg.len ? ld_fresh(sa + seg.start + g) : 0u;
+    }
+    Scratch s{};
+    s.sa = sa;
+    uint32_t tt;
+    if (seg.len <= 64) tt = wave_sort_pre_text<1>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    else if (seg.len <= 128) tt = wave_sort_pre_text<2>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    else if (seg.len <= 256) tt = wave_sort_pre_text<4>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    else tt = wave_sort_pre_text<8>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    tt = uniform(tt);
+    uint32_t D = d + kLdsKeyBytes;
+    while (tt) {
+        if (D + kLdsTieBytes > (uint32_t)kTextDcap) {
+            if (lane == 0) atomicOr(&L.fail, 1u);
+            return;
+        }
+        tt = uniform(lds_tie_round_any(Tl, n, s, seg.start, tt, D, out, orig, W));
+        D += kLdsTieBytes;
+    }
+}
+
+// partition a segment of > kSmall rotations with a common prefix of d bytes
+// by byte d (one wave): children of one rotation are final, runs of small
+// ones go to the queue as batches, large ones as items of depth d+1
+__device__ void text_partition(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* spill, Seg seg, uint32_t d,
+                               uint8_t* out, uint32_t* orig, uint32_t* W, TextLds& L, int nxt) {
+    const int lane = lane_id();
+    uint32_t* hist = W;        // then the batch starts
+    uint32_t* base = W + 256;  // then pack scratch / the batch lengths
+    constexpr int U = 8;
+    const uint32_t rounds = (seg.len + 63) / 64;
+    uint32_t c[4];
+    for (;;) {
+        if (d >= (uint32_t)kTextDcap) {
+            if (lane == 0) atomicOr(&L.fail, 1u);
+            return;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hist[lane * 4 + j] = 0;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t r0 = 0; r0 < rounds; r0 += U) {
+            uint32_t iv[U], cv[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const uint32_t k = (r0 + j) * 64 + lane;
+                iv[j] = k < seg.len ? ld_fresh(sa + seg.start + k) : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const uint32_t k = (r0 + j) * 64 + lane;
+                uint32_t p = iv[j] + d;
+                if (p >= (uint32_t)n) p %= (uint32_t)n;
+                cv[j] = k < seg.len ? (uint32_t)Tl[p] : 0u;
+                if (k < seg.len) spill[seg.start + k] = iv[j] | (cv[j] << 24);
+            }
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const uint32_t k = (r0 + j) * 64 + lane;
+                const bool v = k < seg.len;
+                const uint64_t peers = wave_match8(cv[j], v);
+                if (v && (peers & __lanemask_lt()) == 0) atomicAdd(&hist[cv[j]], (uint32_t)__popcll(peers));
+            }
+        }
+        wave_sync_mem();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = hist[lane * 4 + j];
+        bool one = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) one |= c[j] == seg.len;
+        if (!__ballot(one)) break;
+        d++;  // every rotation has the same byte here: one level deeper, nothing moves
+    }
+    uint32_t ex[4], tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        ex[j] = tot;
+        tot += c[j];
+    }
+    const uint32_t lex = wave_incl_sum(tot) - tot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        ex[j] += lex;
+        base[lane * 4 + j] = ex[j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t k = r * 64 + lane;
+        const bool v = k < seg.len;
+        const uint32_t x = v ? ld_fresh(spill + seg.start + k) : 0u;
+        const uint32_t cc = x >> 24;
+        const uint64_t peers = wave_match8(cc, v);
+        const uint64_t below = peers & __lanemask_lt();
+        const int leader = peers ? __builtin_ctzll(peers) : 0;
+        uint32_t bs = 0;
+        if (v && below == 0) bs = atomicAdd(&base[cc], (uint32_t)__popcll(peers));
+        bs = (uint32_t)__shfl((int)bs, leader);
+        if (v) sa[seg.start + bs + (uint32_t)__popcll(below)] = x & 0xffffffu;
+    }
+    wave_sync_mem();  // the scatter is visible to the reads below
+    // batches of the small children (pack scratch: the hist and base areas)
+    const uint32_t nbat = pack_children_wave(hist, base, W + 512, hist, base);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (c[j] == 1u) {
+            const uint32_t pos = seg.start + ex[j];
+            text_final(Tl, n, pos, ld_fresh(sa + pos), out, orig);
+        }
+    }
+    bool big[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) big[j] = c[j] > (uint32_t)kSmall;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tq_push(L, nxt, big[j], seg.start + ex[j], c[j], d + 1);
+    for (uint32_t k0 = 0; k0 < nbat; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool v = k < nbat;
+        const uint32_t bl = v ? base[k] : 0u;
+        const uint32_t bst = v ? hist[k] : 0u;
+        tq_push(L, nxt, v, seg.start + bst, bl & 0x7fffffffu, d + (bl >> 31));
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                      const uint32_t* __restrict__ lens, int nblocks,
+                                                      uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                      uint32_t* __restrict__ orig_out,
+                                                      const uint32_t* __restrict__ present, uint32_t* __restrict__ redo,
+                                                      uint32_t* __restrict__ spill_all, Seg* __restrict__ grp_all) {
+    __shared__ TextLds L;
+    const int b = blockIdx.x;
+    if (b >= nblocks || redo[b] != 1u) return;
+    const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+    const int n = (int)uniform(lens[b]);
+    const uint8_t* T = blocks + (size_t)b * stride;
+    uint8_t* out = bwt_out + (size_t)b * stride;
+    uint32_t* orig = orig_out + b;
+    uint32_t* sa = sa_all + (size_t)b * stride;
+    uint32_t* spill = spill_all + (size_t)b * stride;
+    // pair-bucket starts, row-major over dense ids (K*K + 1 words)
+    uint32_t* pst = reinterpret_cast<uint32_t*>(grp_all + (size_t)b * bwt_group_stride(stride));
+    const uint8_t* Tl = reinterpret_cast<const uint8_t*>(L.text);
+    {
+        const int n16 = (n + 15) >> 4;
+        const uint4* T4 = reinterpret_cast<const uint4*>(T);
+        for (int v = t; v < n16; v += FT) L.text[v] = T4[v];
+    }
+    // dense ids of the bytes in use (the symbol map of bwt_block_kernel mode 0)
+    uint32_t K;
+    {
+        const uint32_t pw = t < 8 ? present[(size_t)b * 8 + t] : 0u;
+        if (t < 8) L.tmp[t] = pw;
+        __syncthreads();
+        if (t < 256) {
+            uint32_t below = 0;
+            for (int q = 0; q < (t >> 5); ++q) below += (uint32_t)__popc(L.tmp[q]);
+            below += (uint32_t)__popc(L.tmp[t >> 5] & ((1u << (t & 31)) - 1u));
+            L.id[t] = (uint8_t)below;
+        }
+        uint32_t k = 0;
+        for (int q = 0; q < 8; ++q) k += (uint32_t)__popc(L.tmp[q]);
+        K = uniform(k);
+    }
+    const uint32_t KK = K * K;
+    for (uint32_t e = t; e < KK; e += FT) L.u.cur[e] = 0;
+    if (t == 0) L.fail = 0;
+    __syncthreads();
+    // ---- pair histogram, starts, scatter of every rotation into its pair bucket
+    for (int i = t; i < n; i += FT) {
+        const uint32_t a = L.id[Tl[i]], c2 = L.id[Tl[i + 1 < n ? i + 1 : 0]];
+        atomicAdd(&L.u.cur[a * K + c2], 1u);
+    }
+    __syncthreads();
+    {
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t e = (uint32_t)t * 4 + j;
+            v[j] = e < KK ? L.u.cur[e] : 0u;
+            sum += v[j];
+        }
+        uint32_t total;
+        uint32_t run = wg_excl_sum<FT>(sum, L.tmp, &total);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t e = (uint32_t)t * 4 + j;
+            if (e < KK) {
+                L.u.cur[e] = run;
+                pst[e] = run;
+                if (e % K == 0) L.cstart[e / K] = run;
+            }
+            run += v[j];
+        }
+        if (t == 0) {
+            pst[KK] = (uint32_t)n;
+            L.cstart[K] = (uint32_t)n;
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += FT) {
+        const uint32_t a = L.id[Tl[i]], c2 = L.id[Tl[i + 1 < n ? i + 1 : 0]];
+        sa[atomicAdd(&L.u.cur[a * K + c2], 1u)] = (uint32_t)i;
+    }
+    // processing order: ascending first-byte bucket size (ties by byte)
+    if (t < 64) {
+        const uint32_t me = (uint32_t)t < K ? L.cstart[t + 1] - L.cstart[t] : 0xffffffffu;
+        uint32_t rk = 0;
+        for (uint32_t q = 0; q < K; ++q) {
+            const uint32_t o = L.cstart[q + 1] - L.cstart[q];
+            rk += (o < me || (o == me && q < (uint32_t)t)) ? 1u : 0u;
+        }
+        if ((uint32_t)t < K) {
+            L.order[rk] = (uint8_t)t;
+            L.done[t] = 0;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    uint32_t* W = L.u.w[w];
+    for (uint32_t s = 0; s < K; ++s) {
+        const uint32_t ss = L.order[s];
+        // ---- sort phase: the pair buckets (ss, b) not filled by earlier
+        // copies, in rounds: every wave takes items of the round's list
+        // round-robin, partitions put their children into the next round's
+        if (t < 2) L.qn[t] = 0;
+        __syncthreads();
+        if (w == 0) {
+            const bool in = (uint32_t)lane < K;
+            const uint32_t st = in ? pst[ss * K + lane] : 0u, en = in ? pst[ss * K + lane + 1] : 0u;
+            const uint32_t len = en - st;
+            const bool expl = in && len > 0 && ((uint32_t)lane == ss || !L.done[lane]);
+            if (expl && len == 1) text_final(Tl, n, st, ld_fresh(sa + st), out, orig);
+            tq_push(L, 0, expl && len >= 2, st, len, 2);
+            // copy targets: unprocessed x != ss with rotations "x ss"
+            const bool tg = in && (uint32_t)lane != ss && !L.done[lane] &&
+                            pst[lane * K + ss + 1] > pst[lane * K + ss];
+            if (in) {
+                L.target[lane] = tg ? 1 : 0;
+                L.pcol[lane] = pst[lane * K + ss];
+            }
+        }
+        __syncthreads();
+        for (int cur = 0;; cur ^= 1) {
+            const uint32_t nit = min(L.qn[cur], (uint32_t)kTQ);
+            if (nit == 0 || L.fail) break;
+            __syncthreads();  // every thread has read the count
+            if (t == 0) L.qn[cur ^ 1] = 0;
+            __syncthreads();
+            for (uint32_t k = (uint32_t)w; k < nit; k += FW) {
+                const uint64_t it = L.q[cur][k];
+                const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
+                const uint32_t d = uniform((uint32_t)(it >> 34) & 0xffffu);
+                if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, d, out, orig, W, L);
+                else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, cur ^ 1);
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+        __syncthreads();
+        if (L.fail) break;
+        // ---- copy phase: bucket ss is in order; (x, ss) = the rotations i-1 of
+        // it with T[i-1] = x, in that order, for every unprocessed x != ss
+        bool any = false;
+        for (uint32_t x = 0; x < K; ++x) any |= L.target[x] != 0;
+        if (any) {
+            const uint32_t cs = L.cstart[ss], ce = L.cstart[ss + 1];
+            const uint32_t per = ((ce - cs + FW - 1) / FW + 63) & ~63u;
+            const uint32_t w0 = min(ce, cs + per * (uint32_t)w), w1 = min(ce, w0 + per);
+            W[lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t k = w0 + lane; k < w1; k += 64) {
+                const uint32_t i = ld_fresh(sa + k);
+                const uint32_t x = L.id[Tl[i ? i - 1 : (uint32_t)n - 1]];
+                if (L.target[x]) atomicAdd(&W[x], 1u);
+            }
+            __syncthreads();
+            if ((uint32_t)t < K) {
+                uint32_t run = L.pcol[t];
+                for (int q = 0; q < FW; ++q) {
+                    const uint32_t v = L.u.w[q][t];
+                    L.u.w[q][t] = run;
+                    run += v;
+                }
+            }
+            __syncthreads();
+            for (uint32_t k0 = w0; k0 < w1; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                const bool v = k < w1;
+                const uint32_t i = v ? ld_fresh(sa + k) : 0u;
+                const uint32_t j = i ? i - 1 : (uint32_t)n - 1;
+                const uint32_t x = v ? L.id[Tl[j]] : 0u;
+                const bool tg = v && L.target[x];
+                const uint64_t peers = wave_match6(x, tg);
+                const uint32_t bs = W[x];
+                if (tg) {
+                    const uint32_t pos = bs + (uint32_t)__popcll(peers & __lanemask_lt());
+                    sa[pos] = j;
+                    text_final(Tl, n, pos, j, out, orig);
+                    if ((peers & __lanemask_lt()) == 0) W[x] = bs + (uint32_t)__popcll(peers);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        if (t == 0) L.done[ss] = 1;
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (t == 0 && L.fail) redo[b] = 2u;
+}
+
+// BZ2MI_TEXTBWT=0 (A/B): the text-like blocks go through the general path
+__global__ void redo_all_kernel(uint32_t* redo, int nblocks) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nblocks && redo[b] == 1u) redo[b] = 2u;
 }
 
 // ---- kernel 4 (one launch per round, one workgroup per block): the block's

@@ -31,6 +31,8 @@
 // D_{g-1}) from the block's initial list -- the list the sequential encoder
 // holds at p_g.  Segments are coded concurrently into scratch and then
 // concatenated.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -446,7 +448,11 @@ void launch_mtf(int nb, const uint8_t* bwt, size_t stride, const uint32_t* lens,
     // waves per block: one while the blocks alone fill the chip's SIMDs
     // several times over (each wave's tile chain is latency-bound below ~6
     // waves per SIMD), else segments
-    const int g = nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : 8;
+    static const int force = [] {
+        const char* e = getenv("BZ2MI_MTF_WAVES");  // A/B override: 1, 2, 4 or 8
+        return e ? atoi(e) : 0;
+    }();
+    const int g = force ? force : nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : 8;
 #define BZ2MI_MTF_LAUNCH(G)                                                                                     \
     hipLaunchKernelGGL(mtf_kernel<G>, dim3(nb), dim3(64 * G), 0, s, bwt, stride, lens, nb, present, mtf_out,      \
                        mtf_stride, mtf_len, alpha_out, hist_out, scratch, scratch_stride)
