@@ -846,7 +846,7 @@ int bz2mi_compress_device(bz2mi_ctx* c, const void* d_in, size_t n, void* d_out,
 
 // phase stamps of the representative workgroup of the last launch (builds
 // with PHASES=1; returns 0 otherwise): kernel 0 = huffman, 1 = bwt, 2 = mtf,
-// 3 = front end
+// 3 = front end, 4 = text BWT sums
 int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
     if (!out16) return BZ2MI_EINVAL;
     switch (kernel) {
@@ -854,6 +854,7 @@ int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
         case 1: return bz2mi::bwt_phases(out16);
         case 2: return bz2mi::mtf_phases(out16);
         case 3: return bz2mi::fe_phases(out16);
+        case 4: return bz2mi::tbk_stats(out16);
         default: return BZ2MI_EINVAL;
     }
 }

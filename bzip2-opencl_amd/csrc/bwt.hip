@@ -30,6 +30,18 @@
 namespace bz2mi {
 
 BZ2MI_PHASE_TABLE(g_bwt_phase)
+BZ2MI_PHASE_TABLE(g_tbk_stat)
+
+// PHASES builds: bwt_text_kernel sums over all its blocks (wall clock of
+// thread 0 in 10 ns units for 0..2, counts for the rest)
+int tbk_stats(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbk_stat), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
+    (void)out;
+    return 0;
+#endif
+}
 
 int bwt_phases(unsigned long long* out) {
 #ifdef BZ2MI_PHASES
@@ -2319,6 +2331,7 @@ __global__ __launch_bounds__(FT) void bwt_block_small_kernel(const uint8_t* __re
 // general path (bwt_block_kernel mode 1).
 constexpr int kTextDcap = 512;   // depth at which a tie or a partition gives up
 
+constexpr int kTextChain = 32;    // levels a partition goes down with one child before the block is handed back
 constexpr int kTQ = 512;         // work items per round
 constexpr int kTW = 768;         // per-wave LDS words
 
@@ -2332,19 +2345,20 @@ struct TextLds {
     uint32_t pcol[kTextAlpha];        // start of (x, ss) for the copy targets
     uint32_t cstart[kTextAlpha + 1];  // first-byte bucket starts
     uint32_t tmp[FW];
-    uint32_t qn[2], fail;
+    uint32_t qn[2], fail, claim;
     uint8_t id[256];                  // byte -> dense id
     uint8_t order[kTextAlpha];        // ids by ascending bucket size
-    uint8_t done[kTextAlpha];
+    uint8_t rank[kTextAlpha];         // position of an id in that order
     uint8_t target[kTextAlpha];
 };
 
-// SA / spill words the text kernel reads back after other waves (or this
-// one) rewrote them within the launch: device-coherent loads that bypass the
-// CU's vector L1, which may still hold the line from an earlier read
-__device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// SA / spill words the text kernel reads back after this wave or another of
+// the workgroup rewrote them: plain loads.  The waves of a workgroup share the
+// CU's vector L1, which keeps their stores and loads in order, so the
+// workgroup fences / barriers in between are all the ordering needed.  (An
+// L1-bypassing agent-scope load here can overtake the wave's own earlier
+// store: it read stale spill words.)
+__device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) { return *p; }
 
 __device__ __forceinline__ uint64_t tq_item(uint32_t start, uint32_t len, uint32_t depth) {
     return ((uint64_t)(depth & 0xffffu) << 34) | ((uint64_t)len << 17) | (uint64_t)start;  // start, len < 2^17
@@ -2378,6 +2392,32 @@ __device__ __forceinline__ uint64_t wave_match6(uint32_t key, bool valid) {
     return peers;
 }
 
+#ifdef TBK_CHECK
+#define TBK_ASSERT(cond, what, a, b)                                                                  \
+    do {                                                                                              \
+        if (!(cond)) {                                                                                \
+            if (lane_id() == 0) printf("[tbk] block %d wave %d: %s (%u, %u)\n", (int)blockIdx.x,       \
+                                       (int)(threadIdx.x >> 6), what, (unsigned)(a), (unsigned)(b)); \
+            if (lane_id() == 0) atomicOr(&L.fail, 1u);                                                \
+            return;                                                                                   \
+        }                                                                                             \
+    } while (0)
+#else
+#define TBK_ASSERT(cond, what, a, b) \
+    do {                             \
+    } while (0)
+#endif
+#ifdef BZ2MI_PHASES
+#define TBK_COUNT(k, v)                                                             \
+    do {                                                                            \
+        if (lane_id() == 0) atomicAdd(&g_tbk_stat[k], (unsigned long long)(v));     \
+    } while (0)
+#else
+#define TBK_COUNT(k, v) \
+    do {                \
+    } while (0)
+#endif
+
 // a rotation's final position: its BWT byte (and origPtr)
 __device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t pos, uint32_t i, uint8_t* out,
                                            uint32_t* orig) {
@@ -2387,10 +2427,21 @@ __device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t po
 
 // sort a segment of <= kSmall rotations with a common prefix of d bytes (one
 // wave; keys from the LDS text); final SA entries, BWT bytes, origPtr
-__device__ void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out, uint32_t* orig,
+#ifndef TBK_SORT_INL
+#define TBK_SORT_INL __forceinline__
+#endif
+// text_partition stays a call: inlined into the kernel (80 SGPRs spilled)
+// the periodic golden block fb_const -9 hangs the kernel, as a call it does
+// not (its LDS accesses are then FLAT)
+#ifndef TBK_PART_INL
+#define TBK_PART_INL __noinline__
+#endif
+__device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out, uint32_t* orig,
                           uint32_t* W, TextLds& L) {
     constexpr int E = kSmall / 64;
     const int lane = lane_id();
+    TBK_ASSERT(seg.start + seg.len <= (uint32_t)n && seg.len >= 2u && seg.len <= (uint32_t)kSmall, "sort seg", seg.start,
+               seg.len);
     uint32_t pre[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -2405,8 +2456,11 @@ __device__ void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint3
     else if (seg.len <= 256) tt = wave_sort_pre_text<4>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
     else tt = wave_sort_pre_text<8>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
     tt = uniform(tt);
+    TBK_COUNT(4, 1);
+    TBK_COUNT(7, seg.len);
     uint32_t D = d + kLdsKeyBytes;
     while (tt) {
+        TBK_COUNT(10, 1);
         if (D + kLdsTieBytes > (uint32_t)kTextDcap) {
             if (lane == 0) atomicOr(&L.fail, 1u);
             return;
@@ -2419,19 +2473,23 @@ __device__ void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint3
 // partition a segment of > kSmall rotations with a common prefix of d bytes
 // by byte d (one wave): children of one rotation are final, runs of small
 // ones go to the queue as batches, large ones as items of depth d+1
-__device__ void text_partition(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* spill, Seg seg, uint32_t d,
+__device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* spill, Seg seg, uint32_t d,
                                uint8_t* out, uint32_t* orig, uint32_t* W, TextLds& L, int nxt) {
     const int lane = lane_id();
     uint32_t* hist = W;        // then the batch starts
     uint32_t* base = W + 256;  // then pack scratch / the batch lengths
     constexpr int U = 8;
     const uint32_t rounds = (seg.len + 63) / 64;
+    TBK_ASSERT(seg.start + seg.len <= (uint32_t)n && seg.len > (uint32_t)kSmall, "partition seg", seg.start, seg.len);
     uint32_t c[4];
+    const uint32_t dcap = min((uint32_t)kTextDcap, d + (uint32_t)kTextChain);
     for (;;) {
-        if (d >= (uint32_t)kTextDcap) {
+        if (d >= dcap) {
             if (lane == 0) atomicOr(&L.fail, 1u);
             return;
         }
+        TBK_COUNT(5, 1);
+        TBK_COUNT(6, seg.len);
 #pragma unroll
         for (int j = 0; j < 4; ++j) hist[lane * 4 + j] = 0;
         __builtin_amdgcn_wave_barrier();
@@ -2474,6 +2532,8 @@ __device__ void text_partition(const uint8_t* Tl, int n, uint32_t* sa, uint32_t*
         tot += c[j];
     }
     const uint32_t lex = wave_incl_sum(tot) - tot;
+    TBK_ASSERT((uint32_t)__builtin_amdgcn_readlane((int)(lex + tot), 63) == seg.len, "partition hist",
+               __builtin_amdgcn_readlane((int)(lex + tot), 63), seg.len);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         ex[j] += lex;
@@ -2491,6 +2551,7 @@ __device__ void text_partition(const uint8_t* Tl, int n, uint32_t* sa, uint32_t*
         uint32_t bs = 0;
         if (v && below == 0) bs = atomicAdd(&base[cc], (uint32_t)__popcll(peers));
         bs = (uint32_t)__shfl((int)bs, leader);
+        TBK_ASSERT(!__ballot(v && bs + (uint32_t)__popcll(below) >= seg.len), "partition scatter", bs, seg.len);
         if (v) sa[seg.start + bs + (uint32_t)__popcll(below)] = x & 0xffffffu;
     }
     wave_sync_mem();  // the scatter is visible to the reads below
@@ -2527,6 +2588,10 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     __shared__ TextLds L;
     const int b = blockIdx.x;
     if (b >= nblocks || redo[b] != 1u) return;
+#ifdef BZ2MI_PHASES
+    const unsigned long long tk0 = wall_clock64();
+    unsigned long long tks = 0, tkc = 0, tk1 = 0;
+#endif
     const int t = threadIdx.x, w = wave_id(), lane = lane_id();
     const int n = (int)uniform(lens[b]);
     const uint8_t* T = blocks + (size_t)b * stride;
@@ -2608,53 +2673,90 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         }
         if ((uint32_t)t < K) {
             L.order[rk] = (uint8_t)t;
-            L.done[t] = 0;
+            L.rank[t] = (uint8_t)rk;
         }
     }
     __threadfence_block();
     __syncthreads();
+#ifdef BZ2MI_PHASES
+    if (t == 0) atomicAdd(&g_tbk_stat[0], wall_clock64() - tk0);
+#endif
     uint32_t* W = L.u.w[w];
-    for (uint32_t s = 0; s < K; ++s) {
-        const uint32_t ss = L.order[s];
-        // ---- sort phase: the pair buckets (ss, b) not filled by earlier
-        // copies, in rounds: every wave takes items of the round's list
-        // round-robin, partitions put their children into the next round's
-        if (t < 2) L.qn[t] = 0;
+    // ---- sort phase: the pair buckets (a, c) with rank(c) >= rank(a) are
+    // sorted directly (the others are filled by the copies below), all at
+    // once: round 0 claims the pair buckets 64 at a time, partitions put
+    // their children into the next round's list; a round ends at a barrier
+#ifdef BZ2MI_PHASES
+    tk1 = wall_clock64();
+#endif
+    if (t < 2) L.qn[t] = 0;
+    if (t == 0) L.claim = 0;
+    __syncthreads();
+    for (;;) {
+        uint32_t e0 = 0;
+        if (lane == 0) e0 = atomicAdd(&L.claim, 64u);
+        e0 = uniform(e0);
+        if (e0 >= KK) break;
+        const uint32_t e = e0 + (uint32_t)lane;
+        const uint32_t a = e / K, c2 = e - a * K;
+        const uint32_t st = e < KK ? pst[e] : 0u, len = e < KK ? pst[e + 1] - st : 0u;
+        const bool expl = e < KK && len > 0 && L.rank[c2] >= L.rank[a];
+        if (expl && len == 1) text_final(Tl, n, st, ld_fresh(sa + st), out, orig);
+        for (uint64_t m = __ballot(expl && len >= 2); m; m &= m - 1) {
+            if (*(volatile uint32_t*)&L.fail) break;  // the block goes back to the general path
+            const int l = __builtin_ctzll(m);
+            const Seg seg{uniform((uint32_t)__shfl((int)st, l)), uniform((uint32_t)__shfl((int)len, l))};
+            if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, 2, out, orig, W, L);
+            else text_partition(Tl, n, sa, spill, seg, 2, out, orig, W, L, 0);
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int cur = 0;; cur ^= 1) {
+        const uint32_t nit = min(L.qn[cur], (uint32_t)kTQ);
+        if (nit == 0 || L.fail) break;
+        if (t == 0) TBK_COUNT(3, 1);
+        __syncthreads();  // every thread has read the count
+        if (t == 0) {
+            L.qn[cur ^ 1] = 0;
+            L.claim = 0;
+        }
         __syncthreads();
+        for (;;) {
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(&L.claim, 1u);
+            k = uniform(k);
+            if (k >= nit || *(volatile uint32_t*)&L.fail) break;
+            const uint64_t it = L.q[cur][k];
+            const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
+            const uint32_t d = uniform((uint32_t)(it >> 34) & 0xffffu);
+            if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, d, out, orig, W, L);
+            else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, cur ^ 1);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    __syncthreads();
+#ifdef BZ2MI_PHASES
+    tks = wall_clock64() - tk1;
+#endif
+    // ---- copy steps in ascending bucket size: bucket ss is complete (its
+    // sorted pair buckets, and (ss, c) for every earlier c from that step's
+    // copy); it fills (x, ss) for every later x
+    for (uint32_t s = 0; s < K && !L.fail; ++s) {
+        const uint32_t ss = L.order[s];
+#ifdef BZ2MI_PHASES
+        tk1 = wall_clock64();
+#endif
         if (w == 0) {
             const bool in = (uint32_t)lane < K;
-            const uint32_t st = in ? pst[ss * K + lane] : 0u, en = in ? pst[ss * K + lane + 1] : 0u;
-            const uint32_t len = en - st;
-            const bool expl = in && len > 0 && ((uint32_t)lane == ss || !L.done[lane]);
-            if (expl && len == 1) text_final(Tl, n, st, ld_fresh(sa + st), out, orig);
-            tq_push(L, 0, expl && len >= 2, st, len, 2);
-            // copy targets: unprocessed x != ss with rotations "x ss"
-            const bool tg = in && (uint32_t)lane != ss && !L.done[lane] &&
-                            pst[lane * K + ss + 1] > pst[lane * K + ss];
+            const bool tg = in && L.rank[lane] > s && pst[lane * K + ss + 1] > pst[lane * K + ss];
             if (in) {
                 L.target[lane] = tg ? 1 : 0;
                 L.pcol[lane] = pst[lane * K + ss];
             }
         }
         __syncthreads();
-        for (int cur = 0;; cur ^= 1) {
-            const uint32_t nit = min(L.qn[cur], (uint32_t)kTQ);
-            if (nit == 0 || L.fail) break;
-            __syncthreads();  // every thread has read the count
-            if (t == 0) L.qn[cur ^ 1] = 0;
-            __syncthreads();
-            for (uint32_t k = (uint32_t)w; k < nit; k += FW) {
-                const uint64_t it = L.q[cur][k];
-                const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
-                const uint32_t d = uniform((uint32_t)(it >> 34) & 0xffffu);
-                if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, d, out, orig, W, L);
-                else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, cur ^ 1);
-            }
-            __threadfence_block();
-            __syncthreads();
-        }
-        __syncthreads();
-        if (L.fail) break;
         // ---- copy phase: bucket ss is in order; (x, ss) = the rotations i-1 of
         // it with T[i-1] = x, in that order, for every unprocessed x != ss
         bool any = false;
@@ -2698,11 +2800,22 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                 __builtin_amdgcn_wave_barrier();
             }
         }
-        if (t == 0) L.done[ss] = 1;
         __threadfence_block();
         __syncthreads();
+#ifdef BZ2MI_PHASES
+        tkc += wall_clock64() - tk1;
+#endif
     }
     if (t == 0 && L.fail) redo[b] = 2u;
+#ifdef BZ2MI_PHASES
+    if (t == 0) {
+        atomicAdd(&g_tbk_stat[1], tks);
+        atomicAdd(&g_tbk_stat[2], tkc);
+        atomicAdd(&g_tbk_stat[8], 1ull);
+        atomicAdd(&g_tbk_stat[9], wall_clock64() - tk0);
+        atomicAdd(&g_tbk_stat[11], (unsigned long long)K);
+    }
+#endif
 }
 
 // BZ2MI_TEXTBWT=0 (A/B): the text-like blocks go through the general path

@@ -1,0 +1,25 @@
+"""Debug: bwt_text_kernel sums over one compression of C3 text (library built
+with `make phases`; run with BZ2MI_LIBRARY=bzip2-opencl_amd/bz2mi/libbz2mi_ph.so)."""
+import ctypes, os, sys
+R = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")
+sys.path.insert(0, os.path.join(R, "bzip2-opencl_amd"))
+import torch
+import bz2mi
+from bz2mi import synth
+
+n = int(os.environ.get("MIB", "256")) << 20
+x = torch.from_numpy(synth.text_bytes(n, synth.SEED_TEXT)).cuda()
+ctx = bz2mi.Context(9, 10)
+out = torch.empty(n + n // 8 + (1 << 20), dtype=torch.uint8, device="cuda")
+ctx.compress_device(x.data_ptr(), n, out.data_ptr(), out.numel())
+torch.cuda.synchronize()
+L = bz2mi.lib()
+buf = (ctypes.c_ulonglong * 16)()
+print("rc", L.bz2mi_debug_phases(4, buf))
+v = list(buf)
+nb = max(1, v[8])
+print(f"blocks {v[8]}  per block: total {v[9] / nb / 100:.1f} us, setup {v[0] / nb / 100:.1f}, sort {v[1] / nb / 100:.1f}, "
+      f"copy {v[2] / nb / 100:.1f};  steps {v[11] / nb:.1f}, rounds {v[3] / nb:.1f}")
+print(f"  sorts {v[4] / nb:.1f} ({v[7] / nb:.0f} elems, tie rounds {v[10] / nb:.1f}), partitions {v[5] / nb:.1f} "
+      f"({v[6] / nb:.0f} elems)")
+print("timings", ctx.timings())
