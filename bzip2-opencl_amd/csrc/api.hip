@@ -859,6 +859,10 @@ int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
     }
 }
 
+// TBK_TRACE builds: the text kernel's waves store their position to this
+// host-mapped buffer (16 words per block); returns 0 in other builds
+int bz2mi_debug_trace(void* host_mapped) { return bz2mi::tbk_trace(host_mapped); }
+
 // device self-test of the cross-lane primitives: fills bad[0..9] with
 // mismatch counts (all zero on a healthy build); returns the number of checks
 int bz2mi_debug_selftest(uint32_t* bad, int n) {

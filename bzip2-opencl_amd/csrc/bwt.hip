@@ -31,9 +31,21 @@ namespace bz2mi {
 
 BZ2MI_PHASE_TABLE(g_bwt_phase)
 BZ2MI_PHASE_TABLE(g_tbk_stat)
+#ifdef TBK_TRACE
+__device__ unsigned int* g_tbk_trace;
+#endif
 
 // PHASES builds: bwt_text_kernel sums over all its blocks (wall clock of
 // thread 0 in 10 ns units for 0..2, counts for the rest)
+int tbk_trace(void* p) {
+#ifdef TBK_TRACE
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tbk_trace), &p, sizeof(p)) == hipSuccess ? 1 : -1;
+#else
+    (void)p;
+    return 0;
+#endif
+}
+
 int tbk_stats(unsigned long long* out) {
 #ifdef BZ2MI_PHASES
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbk_stat), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
@@ -2332,7 +2344,8 @@ __global__ __launch_bounds__(FT) void bwt_block_small_kernel(const uint8_t* __re
 constexpr int kTextDcap = 512;   // depth at which a tie or a partition gives up
 
 constexpr int kTextChain = 32;    // levels a partition goes down with one child before the block is handed back
-constexpr int kTQ = 512;         // work items per round
+constexpr int kTQ = 512;
+constexpr int kCopyR = 4;        // rotations per lane and chunk of a copy step         // work items per round
 constexpr int kTW = 768;         // per-wave LDS words
 
 struct TextLds {
@@ -2345,11 +2358,15 @@ struct TextLds {
     uint32_t pcol[kTextAlpha];        // start of (x, ss) for the copy targets
     uint32_t cstart[kTextAlpha + 1];  // first-byte bucket starts
     uint32_t tmp[FW];
-    uint32_t qn[2], fail, claim;
+    uint32_t qn[2], fail;
     uint8_t id[256];                  // byte -> dense id
     uint8_t order[kTextAlpha];        // ids by ascending bucket size
     uint8_t rank[kTextAlpha];         // position of an id in that order
     uint8_t target[kTextAlpha];
+    uint8_t own[kTextAlpha * kTextAlpha];  // the wave that sorts a pair bucket / a round's item
+#ifdef BZ2MI_PHASES
+    uint32_t stat[16];
+#endif
 };
 
 // SA / spill words the text kernel reads back after this wave or another of
@@ -2392,6 +2409,23 @@ __device__ __forceinline__ uint64_t wave_match6(uint32_t key, bool valid) {
     return peers;
 }
 
+// TBK_TRACE builds: every wave's last position in the text kernel, stored to
+// host-mapped memory (bz2mi_debug_trace) so a host thread can read it while a
+// launch hangs; code = what << 24 | detail
+#ifdef TBK_TRACE
+#define TBK_T(what, detail)                                                                                \
+    do {                                                                                                   \
+        if (g_tbk_trace && lane_id() == 0)                                                                 \
+            __hip_atomic_store(&g_tbk_trace[blockIdx.x * 16 + (threadIdx.x >> 6)],                         \
+                               ((unsigned)(what) << 24) | ((unsigned)(detail) & 0xffffffu), __ATOMIC_RELAXED, \
+                               __HIP_MEMORY_SCOPE_SYSTEM);                                                  \
+    } while (0)
+#else
+#define TBK_T(what, detail) \
+    do {                    \
+    } while (0)
+#endif
+
 #ifdef TBK_CHECK
 #define TBK_ASSERT(cond, what, a, b)                                                                  \
     do {                                                                                              \
@@ -2408,15 +2442,26 @@ __device__ __forceinline__ uint64_t wave_match6(uint32_t key, bool valid) {
     } while (0)
 #endif
 #ifdef BZ2MI_PHASES
-#define TBK_COUNT(k, v)                                                             \
-    do {                                                                            \
-        if (lane_id() == 0) atomicAdd(&g_tbk_stat[k], (unsigned long long)(v));     \
+#define TBK_COUNT(k, v)                                           \
+    do {                                                          \
+        if (lane_id() == 0) atomicAdd(&L.stat[k], (uint32_t)(v)); \
     } while (0)
 #else
 #define TBK_COUNT(k, v) \
     do {                \
     } while (0)
 #endif
+
+// Work of an item for the dealing: a sort ~ its padded size, a partition ~ half
+// its length (one pass, the children are items of their own)
+__device__ __forceinline__ uint32_t text_work(uint32_t len) {
+    return len > (uint32_t)kSmall ? (len >> 1) : len <= 64u ? 64u : len <= 128u ? 128u : len <= 256u ? 256u : 512u;
+}
+// the wave of an item whose work starts at `run` (of `total`): equal shares
+__device__ __forceinline__ uint8_t text_owner(uint32_t run, uint32_t wk, uint32_t total) {
+    const uint64_t mid = (uint64_t)run + (wk >> 1);
+    return (uint8_t)min((uint64_t)(FW - 1), mid * FW / (total ? total : 1u));
+}
 
 // a rotation's final position: its BWT byte (and origPtr)
 __device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t pos, uint32_t i, uint8_t* out,
@@ -2430,11 +2475,8 @@ __device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t po
 #ifndef TBK_SORT_INL
 #define TBK_SORT_INL __forceinline__
 #endif
-// text_partition stays a call: inlined into the kernel (80 SGPRs spilled)
-// the periodic golden block fb_const -9 hangs the kernel, as a call it does
-// not (its LDS accesses are then FLAT)
 #ifndef TBK_PART_INL
-#define TBK_PART_INL __noinline__
+#define TBK_PART_INL __forceinline__
 #endif
 __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out, uint32_t* orig,
                           uint32_t* W, TextLds& L) {
@@ -2460,6 +2502,7 @@ __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, S
     TBK_COUNT(7, seg.len);
     uint32_t D = d + kLdsKeyBytes;
     while (tt) {
+        TBK_T(8, D << 12 | tt);
         TBK_COUNT(10, 1);
         if (D + kLdsTieBytes > (uint32_t)kTextDcap) {
             if (lane == 0) atomicOr(&L.fail, 1u);
@@ -2490,6 +2533,7 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
         }
         TBK_COUNT(5, 1);
         TBK_COUNT(6, seg.len);
+        TBK_T(7, d << 17 | seg.len);
 #pragma unroll
         for (int j = 0; j < 4; ++j) hist[lane * 4 + j] = 0;
         __builtin_amdgcn_wave_barrier();
@@ -2624,6 +2668,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         K = uniform(k);
     }
     const uint32_t KK = K * K;
+#ifdef BZ2MI_PHASES
+    if (t < 16) L.stat[t] = 0;
+#endif
     for (uint32_t e = t; e < KK; e += FT) L.u.cur[e] = 0;
     if (t == 0) L.fail = 0;
     __syncthreads();
@@ -2682,56 +2729,112 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     if (t == 0) atomicAdd(&g_tbk_stat[0], wall_clock64() - tk0);
 #endif
     uint32_t* W = L.u.w[w];
+    TBK_T(1, K);
     // ---- sort phase: the pair buckets (a, c) with rank(c) >= rank(a) are
     // sorted directly (the others are filled by the copies below), all at
-    // once: round 0 claims the pair buckets 64 at a time, partitions put
+    // once: round 0 deals the pair buckets over the waves, partitions put
     // their children into the next round's list; a round ends at a barrier
 #ifdef BZ2MI_PHASES
     tk1 = wall_clock64();
 #endif
     if (t < 2) L.qn[t] = 0;
-    if (t == 0) L.claim = 0;
     __syncthreads();
-    for (;;) {
-        uint32_t e0 = 0;
-        if (lane == 0) e0 = atomicAdd(&L.claim, 64u);
-        e0 = uniform(e0);
-        if (e0 >= KK) break;
+    {
+        // deal the pair buckets to the waves in equal shares of work
+        uint32_t wk[4], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t e = (uint32_t)t * 4 + j;
+            wk[j] = 0;
+            if (e < KK) {
+                const uint32_t a = e / K, c2 = e - a * K, len = pst[e + 1] - pst[e];
+                if (len >= 2 && L.rank[c2] >= L.rank[a]) wk[j] = text_work(len);
+            }
+            sum += wk[j];
+        }
+        uint32_t total;
+        uint32_t run = wg_excl_sum<FT>(sum, L.tmp, &total);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t e = (uint32_t)t * 4 + j;
+            if (e < KK) L.own[e] = wk[j] ? text_owner(run, wk[j], total) : (uint8_t)(e % FW);
+            run += wk[j];
+        }
+    }
+    __syncthreads();
+    for (uint32_t e0 = 0; e0 < KK; e0 += 64) {  // scalar loop over the pair buckets
         const uint32_t e = e0 + (uint32_t)lane;
+        const bool mine = e < KK && L.own[e] == (uint8_t)w;
+        if (!__ballot(mine)) continue;
         const uint32_t a = e / K, c2 = e - a * K;
-        const uint32_t st = e < KK ? pst[e] : 0u, len = e < KK ? pst[e + 1] - st : 0u;
-        const bool expl = e < KK && len > 0 && L.rank[c2] >= L.rank[a];
+        const uint32_t st = mine ? pst[e] : 0u, len = mine ? pst[e + 1] - st : 0u;
+        const bool expl = mine && len > 0 && L.rank[c2] >= L.rank[a];
         if (expl && len == 1) text_final(Tl, n, st, ld_fresh(sa + st), out, orig);
         for (uint64_t m = __ballot(expl && len >= 2); m; m &= m - 1) {
-            if (*(volatile uint32_t*)&L.fail) break;  // the block goes back to the general path
+            if (uniform(*(volatile uint32_t*)&L.fail)) break;  // the block goes back to the general path
             const int l = __builtin_ctzll(m);
             const Seg seg{uniform((uint32_t)__shfl((int)st, l)), uniform((uint32_t)__shfl((int)len, l))};
+            TBK_T(2, seg.len);
+#ifdef BZ2MI_PHASES
+            const unsigned long long ti0 = wall_clock64();
+#endif
             if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, 2, out, orig, W, L);
             else text_partition(Tl, n, sa, spill, seg, 2, out, orig, W, L, 0);
+            TBK_T(10, seg.len);
+#ifdef BZ2MI_PHASES
+            TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
+#endif
         }
     }
     __threadfence_block();
     __syncthreads();
     for (int cur = 0;; cur ^= 1) {
-        const uint32_t nit = min(L.qn[cur], (uint32_t)kTQ);
-        if (nit == 0 || L.fail) break;
+        // loop conditions from LDS go through readfirstlane: scalar branches
+        // (a vector-condition loop around the item calls lost the exec mask)
+        const uint32_t nit = uniform(min(L.qn[cur], (uint32_t)kTQ));
+        if (nit == 0 || uniform(L.fail)) break;
         if (t == 0) TBK_COUNT(3, 1);
+        TBK_T(4, cur << 16 | nit);
         __syncthreads();  // every thread has read the count
-        if (t == 0) {
-            L.qn[cur ^ 1] = 0;
-            L.claim = 0;
+        if (t == 0) L.qn[cur ^ 1] = 0;
+        if (w == 0) {  // deal the round's items in equal shares of work
+            uint32_t wk[kTQ / 64], sum = 0;
+#pragma unroll
+            for (int j = 0; j < kTQ / 64; ++j) {
+                const uint32_t k = (uint32_t)lane * (kTQ / 64) + j;
+                wk[j] = k < nit ? text_work((uint32_t)(L.q[cur][k] >> 17) & 0x1ffffu) : 0u;
+                sum += wk[j];
+            }
+            const uint32_t inc = wave_incl_sum(sum);
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            uint32_t run = inc - sum;
+#pragma unroll
+            for (int j = 0; j < kTQ / 64; ++j) {
+                const uint32_t k = (uint32_t)lane * (kTQ / 64) + j;
+                if (k < nit) L.own[k] = text_owner(run, wk[j], total);
+                run += wk[j];
+            }
         }
         __syncthreads();
-        for (;;) {
-            uint32_t k = 0;
-            if (lane == 0) k = atomicAdd(&L.claim, 1u);
-            k = uniform(k);
-            if (k >= nit || *(volatile uint32_t*)&L.fail) break;
+        for (uint32_t k0 = 0; k0 < nit; k0 += 64) {
+            const bool mine = k0 + (uint32_t)lane < nit && L.own[k0 + lane] == (uint8_t)w;
+            for (uint64_t mm = __ballot(mine); mm; mm &= mm - 1) {
+            const uint32_t k = k0 + (uint32_t)__builtin_ctzll(mm);
+            if (uniform(*(volatile uint32_t*)&L.fail)) break;
             const uint64_t it = L.q[cur][k];
             const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
             const uint32_t d = uniform((uint32_t)(it >> 34) & 0xffffu);
+            TBK_T(3, seg.len);
+#ifdef BZ2MI_PHASES
+            const unsigned long long ti0 = wall_clock64();
+#endif
             if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, d, out, orig, W, L);
             else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, cur ^ 1);
+            TBK_T(11, seg.len);
+#ifdef BZ2MI_PHASES
+            TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
+#endif
+            }
         }
         __threadfence_block();
         __syncthreads();
@@ -2743,8 +2846,10 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     // ---- copy steps in ascending bucket size: bucket ss is complete (its
     // sorted pair buckets, and (ss, c) for every earlier c from that step's
     // copy); it fills (x, ss) for every later x
-    for (uint32_t s = 0; s < K && !L.fail; ++s) {
+    const uint32_t failed = uniform(L.fail);
+    for (uint32_t s = 0; s < K && !failed; ++s) {
         const uint32_t ss = L.order[s];
+        TBK_T(5, s);
 #ifdef BZ2MI_PHASES
         tk1 = wall_clock64();
 #endif
@@ -2758,46 +2863,61 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         }
         __syncthreads();
         // ---- copy phase: bucket ss is in order; (x, ss) = the rotations i-1 of
-        // it with T[i-1] = x, in that order, for every unprocessed x != ss
+        // it with T[i-1] = x, in that order, for every later x.  Chunks of
+        // FW * kCopyR * 64 rotations: every wave loads its kCopyR * 64 at once,
+        // counts its targets per x, a scan over the waves gives each wave its
+        // first slot per x (carried from chunk to chunk in pcol), then the
+        // stable placement from registers
         bool any = false;
         for (uint32_t x = 0; x < K; ++x) any |= L.target[x] != 0;
-        if (any) {
+        if (uniform(any ? 1u : 0u)) {
             const uint32_t cs = L.cstart[ss], ce = L.cstart[ss + 1];
-            const uint32_t per = ((ce - cs + FW - 1) / FW + 63) & ~63u;
-            const uint32_t w0 = min(ce, cs + per * (uint32_t)w), w1 = min(ce, w0 + per);
-            W[lane] = 0;
-            __builtin_amdgcn_wave_barrier();
-            for (uint32_t k = w0 + lane; k < w1; k += 64) {
-                const uint32_t i = ld_fresh(sa + k);
-                const uint32_t x = L.id[Tl[i ? i - 1 : (uint32_t)n - 1]];
-                if (L.target[x]) atomicAdd(&W[x], 1u);
-            }
-            __syncthreads();
-            if ((uint32_t)t < K) {
-                uint32_t run = L.pcol[t];
-                for (int q = 0; q < FW; ++q) {
-                    const uint32_t v = L.u.w[q][t];
-                    L.u.w[q][t] = run;
-                    run += v;
-                }
-            }
-            __syncthreads();
-            for (uint32_t k0 = w0; k0 < w1; k0 += 64) {
-                const uint32_t k = k0 + lane;
-                const bool v = k < w1;
-                const uint32_t i = v ? ld_fresh(sa + k) : 0u;
-                const uint32_t j = i ? i - 1 : (uint32_t)n - 1;
-                const uint32_t x = v ? L.id[Tl[j]] : 0u;
-                const bool tg = v && L.target[x];
-                const uint64_t peers = wave_match6(x, tg);
-                const uint32_t bs = W[x];
-                if (tg) {
-                    const uint32_t pos = bs + (uint32_t)__popcll(peers & __lanemask_lt());
-                    sa[pos] = j;
-                    text_final(Tl, n, pos, j, out, orig);
-                    if ((peers & __lanemask_lt()) == 0) W[x] = bs + (uint32_t)__popcll(peers);
+            for (uint32_t c0 = cs; c0 < ce; c0 += FW * kCopyR * 64) {
+                const uint32_t w0 = c0 + (uint32_t)w * (kCopyR * 64);
+                uint32_t jv[kCopyR], xv[kCopyR];
+                W[lane] = 0;
+#pragma unroll
+                for (int r = 0; r < kCopyR; ++r) {
+                    const uint32_t k = w0 + (uint32_t)(r * 64 + lane);
+                    jv[r] = k < ce ? ld_fresh(sa + k) : 0xffffffffu;
                 }
                 __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int r = 0; r < kCopyR; ++r) {
+                    const bool v = jv[r] != 0xffffffffu;
+                    const uint32_t j = jv[r] ? jv[r] - 1 : (uint32_t)n - 1;
+                    const uint32_t x = v ? L.id[Tl[j]] : 0u;
+                    const bool tg = v && L.target[x];
+                    jv[r] = j;
+                    xv[r] = tg ? x : 0xffu;
+                    if (tg) atomicAdd(&W[x], 1u);
+                }
+                __syncthreads();
+                if ((uint32_t)t < K) {
+                    uint32_t run = L.pcol[t];
+                    for (int q = 0; q < FW; ++q) {
+                        const uint32_t v = L.u.w[q][t];
+                        L.u.w[q][t] = run;
+                        run += v;
+                    }
+                    L.pcol[t] = run;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < kCopyR; ++r) {
+                    const uint32_t x = xv[r];
+                    const bool tg = x != 0xffu;
+                    const uint64_t peers = wave_match6(x, tg);
+                    const uint32_t bs = tg ? W[x] : 0u;
+                    if (tg) {
+                        const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
+                        const uint32_t pos = bs + below;
+                        sa[pos] = jv[r];
+                        text_final(Tl, n, pos, jv[r], out, orig);
+                        if (below == 0) W[x] = bs + (uint32_t)__popcll(peers);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
             }
         }
         __threadfence_block();
@@ -2807,6 +2927,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #endif
     }
     if (t == 0 && L.fail) redo[b] = 2u;
+    TBK_T(6, L.fail);
 #ifdef BZ2MI_PHASES
     if (t == 0) {
         atomicAdd(&g_tbk_stat[1], tks);
@@ -2814,6 +2935,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         atomicAdd(&g_tbk_stat[8], 1ull);
         atomicAdd(&g_tbk_stat[9], wall_clock64() - tk0);
         atomicAdd(&g_tbk_stat[11], (unsigned long long)K);
+        for (int k = 3; k < 8; ++k) atomicAdd(&g_tbk_stat[k], (unsigned long long)L.stat[k]);
+        for (int k = 10; k < 14; ++k)
+            if (k != 11) atomicAdd(&g_tbk_stat[k], (unsigned long long)L.stat[k]);
     }
 #endif
 }

@@ -100,6 +100,7 @@ int bwt_phases(unsigned long long* out);
 int mtf_phases(unsigned long long* out);
 int fe_phases(unsigned long long* out);
 int tbk_stats(unsigned long long* out);
+int tbk_trace(void* host_mapped);
 int run_selftest(uint32_t* host_bad, int n);  // cross-lane primitive checks
 int huffman_threads();  // workgroup size of huffman_kernel
 __global__ void huffman_kernel(const uint16_t* mtf, size_t mtf_stride, const uint32_t* mtf_len,

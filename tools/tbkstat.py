@@ -22,4 +22,6 @@ print(f"blocks {v[8]}  per block: total {v[9] / nb / 100:.1f} us, setup {v[0] / 
       f"copy {v[2] / nb / 100:.1f};  steps {v[11] / nb:.1f}, rounds {v[3] / nb:.1f}")
 print(f"  sorts {v[4] / nb:.1f} ({v[7] / nb:.0f} elems, tie rounds {v[10] / nb:.1f}), partitions {v[5] / nb:.1f} "
       f"({v[6] / nb:.0f} elems)")
+print(f"  wave-busy per block: sorts {v[12] / nb / 100:.1f} us, partitions {v[13] / nb / 100:.1f} us "
+      f"(/16 = {(v[12] + v[13]) / nb / 1600:.1f} us of the sort phase)")
 print("timings", ctx.timings())
