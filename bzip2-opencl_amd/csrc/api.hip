@@ -269,13 +269,13 @@ int stage_huffman(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
 }
 
 int ensure_front(FrontBufs& f, int S, size_t n) {
-    if (n <= f.n_cap && f.d_cost) return BZ2MI_OK;
+    if (n <= f.n_cap && f.d_dmap) return BZ2MI_OK;
     const size_t cap = std::max(n, (size_t)1 << 20);
     const size_t nc = (cap + bz2mi::kFeChunk - 1) / bz2mi::kFeChunk;
     const size_t maxb = (cap + cap / 4) / (size_t)(S - 5) + 8;
     int r;
-    if ((r = dalloc(&f.d_cost, cap + 64))) return r;
     if ((r = dalloc(&f.d_dmap, cap + cap / 4 + 4096))) return r;
+    if ((r = dalloc(&f.d_lane, nc * 64 + 64))) return r;
     if ((r = dalloc(&f.d_summ, nc + 1))) return r;
     if ((r = dalloc(&f.d_rsb, nc + 2))) return r;
     if ((r = dalloc(&f.d_agg, nc / kFeScanTile + 2))) return r;
@@ -300,15 +300,15 @@ int enqueue_front_scan(FrontBufs& f, const uint8_t* d_x, size_t n, hipStream_t s
     if (n == 0) return BZ2MI_OK;
     const uint64_t nc = (n + kFeChunk - 1) / kFeChunk;
     const dim3 g4((unsigned)((nc + 3) / 4));
-    hipLaunchKernelGGL(fe_summary_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, f.d_summ);
+    hipLaunchKernelGGL(fe_summary_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, f.d_summ, f.d_ccost);
     const dim3 gs((unsigned)((nc + kFeScanTile - 1) / kFeScanTile));
     for (int pass = 0; pass < 2; ++pass)
         hipLaunchKernelGGL(fe_runscan_kernel, gs, dim3(kFeScanThreads), 0, s, f.d_summ, nc, f.d_rsb, f.d_agg, pass);
-    hipLaunchKernelGGL(fe_cost_kernel, g4, dim3(256), 0, s, d_x, (uint64_t)n, nc, f.d_summ, f.d_rsb, f.d_cost,
-                       f.d_ccost);
     for (int pass = 0; pass < 2; ++pass)
-        hipLaunchKernelGGL(fe_costscan_kernel, gs, dim3(kFeScanThreads), 0, s, f.d_ccost, nc, f.d_fc, f.d_agg, pass);
-    hipLaunchKernelGGL(fe_dmap_kernel, g4, dim3(256), 0, s, d_x, f.d_cost, (uint64_t)n, nc, f.d_fc, f.d_dmap);
+        hipLaunchKernelGGL(fe_costscan_kernel, gs, dim3(kFeScanThreads), 0, s, f.d_ccost, f.d_summ, f.d_rsb, nc, f.d_fc,
+                           f.d_agg, pass);
+    hipLaunchKernelGGL(fe_dmap_kernel, g4, dim3(256), 0, s, d_x, f.d_summ, f.d_rsb, (uint64_t)n, nc, f.d_fc, f.d_dmap,
+                       f.d_lane);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("front-scan");
     return BZ2MI_OK;
@@ -318,7 +318,7 @@ int run_chain(bz2mi_ctx* c, FrontBufs& f, const uint8_t* d_x, size_t n, size_t n
               uint64_t* nb_out, uint64_t* exit_out, hipStream_t s) {
     using namespace bz2mi;
     const uint64_t nc = (n + kFeChunk - 1) / kFeChunk;
-    hipLaunchKernelGGL(fe_chain_kernel, dim3(1), dim3(kFeChainThreads), 0, s, d_x, f.d_cost, f.d_fc, f.d_summ, f.d_dmap,
+    hipLaunchKernelGGL(fe_chain_kernel, dim3(1), dim3(kFeChainThreads), 0, s, d_x, f.d_lane, f.d_fc, f.d_summ, f.d_dmap,
                        (uint64_t)n, nc, c->S, (uint64_t)n_own, entry, ends ? 1 : 0, f.d_bnd, (uint64_t)f.maxb,
                        f.d_nb);
     HIPCHECK(hipGetLastError());
@@ -330,7 +330,7 @@ int run_chain(bz2mi_ctx* c, FrontBufs& f, const uint8_t* d_x, size_t n, size_t n
     if (hv[0] == 0 || hv[0] > f.maxb || hv[1] != 0)
         return fail(BZ2MI_EDEVICE, "front end produced an invalid block count");
     const uint64_t nb = hv[0];
-    hipLaunchKernelGGL(fe_resolve_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, d_x, f.d_cost, f.d_fc,
+    hipLaunchKernelGGL(fe_resolve_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, d_x, f.d_lane, f.d_fc,
                        f.d_summ, (uint64_t)n, nc, (uint64_t)n_own, entry, f.d_bnd, f.d_nb, f.d_starts);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("front-resolve");

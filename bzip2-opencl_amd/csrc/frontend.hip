@@ -65,40 +65,183 @@ __device__ __forceinline__ void load64(const uint8_t* x, uint64_t n, uint64_t at
     }
 }
 
+// the 64 bytes of lane `l` of a chunk as 16 dwords (zero beyond n)
+__device__ __forceinline__ void load16w(const uint8_t* x, uint64_t n, uint64_t at, uint32_t (&w)[16]) {
+    if (at + 64 <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(x + at);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 a = p[q];
+            w[4 * q] = a.x, w[4 * q + 1] = a.y, w[4 * q + 2] = a.z, w[4 * q + 3] = a.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            uint32_t d = 0;
+            for (int r = 0; r < 4; ++r)
+                if (at + 4 * q + r < n) d |= (uint32_t)x[at + 4 * q + r] << (8 * r);
+            w[q] = d;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[16], int q) { return (w[q >> 2] >> (8 * (q & 3))) & 255u; }
+
+// bit q: byte q of the lane's 64 differs from the byte before it (byte 0:
+// from `prev_last`), by SWAR on the dwords
+__device__ __forceinline__ uint64_t rs_mask(const uint32_t (&w)[16], uint32_t prev_last) {
+    uint64_t m = 0;
+    uint32_t top = prev_last & 255u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t d = w[k];
+        const uint32_t t = d ^ ((d << 8) | top);
+        const uint32_t nz = (((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;
+        const uint32_t bits = ((nz >> 7) & 1u) | ((nz >> 14) & 2u) | ((nz >> 21) & 4u) | ((nz >> 28) & 8u);
+        m |= (uint64_t)bits << (4 * k);
+        top = d >> 24;
+    }
+    return m;
+}
+
+// whether chunk c starts a run (its first byte differs from the byte before it)
+__device__ __forceinline__ bool chunk_starts_run(const uint4* summ, uint64_t c) {
+    return c == 0 || (summ[c].x & 0xffu) != ((summ[c - 1].x >> 8) & 0xffu);
+}
+
+// Per-byte trigger costs (cost(i) of the header comment) of lane `lane`'s 64
+// bytes of chunk c, packed four to a dword; returns the lane's sum.  Called by
+// the whole wave (run starts are scanned across the lanes).  rsbc = rsb[c]
+// (the start of the run that holds the byte before the chunk).
+__device__ __forceinline__ uint64_t lane_rs(const uint32_t (&w)[16], uint64_t c, uint32_t len, bool chunk_rs) {
+    const int lane = lane_id();
+    const uint32_t prev_last = (uint32_t)__shfl_up((int)(w[15] >> 24), 1);
+    uint64_t m = rs_mask(w, prev_last);
+    if (lane == 0) m = (m & ~1ull) | (chunk_rs ? 1ull : 0ull);
+    const int valid = (int)min(64u, len > (uint32_t)lane * 64u ? len - (uint32_t)lane * 64u : 0u);
+    (void)c;
+    return valid >= 64 ? m : (m & ((1ull << valid) - 1ull));
+}
+
+// 1 + the last run start (chunk-relative) in the lanes before this one, 0 if none
+__device__ __forceinline__ uint32_t lane_before(uint64_t m) {
+    const int lane = lane_id();
+    const uint32_t lrs = m ? (uint32_t)lane * 64u + 64u - (uint32_t)__clzll((long long)m) : 0u;  // last start + 1
+    uint32_t xs = lrs;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)xs, d);
+        if (lane >= d) xs = xs > y ? xs : y;
+    }
+    uint32_t before = (uint32_t)__shfl_up((int)xs, 1);
+    if (lane == 0) before = 0;
+    return before;
+}
+
+// run start in effect before the lane's first byte (absolute)
+__device__ __forceinline__ uint64_t lane_run_start(uint64_t m, uint64_t c, uint64_t rsbc) {
+    const uint32_t before = lane_before(m);
+    return before ? c * CH + before - 1 : (c == 0 ? 0 : rsbc);
+}
+
+// the costs of the lane's bytes q < qend from its run-start mask; packed
+// four to a dword when PACK
+template <bool PACK>
+__device__ __forceinline__ uint32_t lane_cost_walk(uint64_t m, uint64_t at, uint64_t cur, uint32_t qend,
+                                                   uint32_t (&packed)[16]) {
+    uint32_t ph = (uint32_t)((at - cur) % 255u);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        uint32_t cst = 0;
+        if ((m >> q) & 1u) {
+            if (at + q > 0) cst = piece_cost(ph);
+            ph = 0;
+        } else if (ph == 254u) {
+            cst = 5;
+        }
+        ph = ph == 254u ? 0u : ph + 1u;
+        cst = (uint32_t)q < qend ? cst : 0u;
+        sum += cst;
+        if constexpr (PACK) {
+            if ((q & 3) == 0) packed[q >> 2] = cst;
+            else packed[q >> 2] |= cst << ((q & 3) * 8);
+        }
+    }
+    return sum;
+}
+
+__device__ __forceinline__ uint32_t lane_costs(const uint32_t (&w)[16], uint64_t c, uint32_t len, bool chunk_rs,
+                                               uint64_t rsbc, uint32_t (&packed)[16], uint32_t* ph0) {
+    const uint64_t at = c * CH + (uint64_t)lane_id() * 64;
+    const uint64_t m = lane_rs(w, c, len, chunk_rs);
+    const uint64_t cur = lane_run_start(m, c, rsbc);
+    *ph0 = (uint32_t)((at - cur) % 255u);
+    const uint32_t qend = len > (uint32_t)lane_id() * 64u ? min(64u, len - (uint32_t)lane_id() * 64u) : 0u;
+    return lane_cost_walk<true>(m, at, cur, qend, packed);
+}
+
+// cost of the first byte of chunk c (c < nc) from the scans alone
+__device__ __forceinline__ uint32_t chunk_first_cost(const uint4* summ, const uint64_t* rsb, uint64_t c) {
+    if (c == 0) return 0;
+    const uint32_t ph = (uint32_t)((c * CH - rsb[c]) % 255u);
+    return chunk_starts_run(summ, c) ? piece_cost(ph) : (ph == 254u ? 5u : 0u);
+}
+
 }  // namespace
 
 // ---- K1: per-chunk run summary
 __global__ __launch_bounds__(256) void fe_summary_kernel(const uint8_t* __restrict__ x, uint64_t n, uint64_t nc,
-                                                         uint4* __restrict__ summ) {
+                                                         uint4* __restrict__ summ, uint32_t* __restrict__ cfree) {
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
     if (c >= nc) return;
     const int lane = lane_id();
     const uint64_t c0 = c * CH;
     const uint32_t len = (uint32_t)min((uint64_t)CH, n - c0);
     const uint64_t at = c0 + (uint64_t)lane * 64;
-    uint8_t v[64];
-    load64(x, n, at, v);
-    const uint32_t prev_last = __shfl_up((uint32_t)v[63], 1);
-    uint32_t first_rs = 0xffffffffu, last_rs = 0;
+    uint32_t w[16];
+    load16w(x, n, at, w);
+    // run starts inside the chunk (pos >= 1)
+    const uint64_t m = lane_rs(w, c, len, false);
+    const uint32_t lfirst = m ? (uint32_t)lane * 64u + (uint32_t)__builtin_ctzll(m) : 0xffffffffu;
+    const uint32_t llast = m ? (uint32_t)lane * 64u + 63u - (uint32_t)__clzll((long long)m) : 0u;
+    uint32_t first_rs = lfirst, last_rs = llast;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        first_rs = min(first_rs, (uint32_t)__shfl_xor((int)first_rs, d));
+        last_rs = max(last_rs, (uint32_t)__shfl_xor((int)last_rs, d));
+    }
+    const uint32_t lead = first_rs == 0xffffffffu ? len : first_rs;
+    // the context-free part of the chunk's cost: the bytes after the first run
+    // start inside the chunk (lead), whose runs all start in the chunk; the
+    // bytes up to lead depend on the run that comes in (fe_costscan_kernel).
+    // Walked as if the chunk's first run started at lead; bytes <= lead dropped.
+    const uint32_t lo = (uint32_t)lane * 64u, before = lane_before(m);
+    uint64_t keep = lead + 1 > lo ? (lead + 1 - lo >= 64 ? 0ull : ~0ull << (lead + 1 - lo)) : ~0ull;  // pos > lead
+    const uint32_t qend = len > lo ? min(64u, len - lo) : 0u;                                         // pos < len
+    keep &= qend >= 64 ? ~0ull : ((1ull << qend) - 1ull);
+    // (a lane after lead has a run start before it; a lane holding lead
+    // restarts its phase there)
+    uint32_t ph = (lo - (before ? before - 1 : 0u)) % 255u;
+    uint32_t fsum = 0;
 #pragma unroll
     for (int q = 0; q < 64; ++q) {
-        const uint32_t pos = (uint32_t)lane * 64 + q;
-        const uint32_t prev = q ? v[q - 1] : prev_last;
-        const bool rs = pos > 0 && pos < len && v[q] != prev;
-        if (rs) {
-            first_rs = min(first_rs, pos);
-            last_rs = pos;
+        uint32_t cst = 0;
+        if ((m >> q) & 1u) {
+            cst = piece_cost(ph);
+            ph = 0;
+        } else if (ph == 254u) {
+            cst = 5;
         }
+        ph = ph == 254u ? 0u : ph + 1u;
+        fsum += ((keep >> q) & 1u) ? cst : 0u;
     }
-    for (int d = 32; d >= 1; d >>= 1) {
-        first_rs = min(first_rs, (uint32_t)__shfl_xor(first_rs, d));
-        last_rs = max(last_rs, (uint32_t)__shfl_xor(last_rs, d));
-    }
+    fsum = wave_sum(fsum);
     if (lane == 0) {
-        const uint32_t lead = first_rs == 0xffffffffu ? len : first_rs;
         const uint32_t trail = len - last_rs;
         const uint32_t fb = x[c0], lb = x[c0 + len - 1];
         summ[c] = make_uint4(fb | (lb << 8), lead, trail, len);
+        cfree[c] = fsum;
     }
 }
 
@@ -194,7 +337,16 @@ __global__ __launch_bounds__(kFeScanThreads) void fe_runscan_kernel(const uint4*
     if (blockIdx.x == 0 && threadIdx.x == 0) rsb[0] = 0;
 }
 
-__global__ __launch_bounds__(kFeScanThreads) void fe_costscan_kernel(const uint32_t* __restrict__ ccost, uint64_t nc,
+// A chunk's cost = its context-free part (fe_summary_kernel) + the part of the
+// run that comes in: with ph0 = (c*CH - rsb[c]) % 255 (the piece position of
+// that run at the chunk start) and L = the chunk's lead, a chunk that starts a
+// run pays the previous run's last piece first and its own first run starts
+// at phase 0; either way the first run completes (p + L) / 255 pieces of 255
+// bytes in the chunk (5 bytes each) and, when it ends inside the chunk, pays
+// its last piece at byte L.
+__global__ __launch_bounds__(kFeScanThreads) void fe_costscan_kernel(const uint32_t* __restrict__ cfree,
+                                                                     const uint4* __restrict__ summ,
+                                                                     const uint64_t* __restrict__ rsb, uint64_t nc,
                                                                      uint64_t* __restrict__ fc,
                                                                      uint64_t* __restrict__ agg, int pass) {
     __shared__ uint64_t wt[kFeScanThreads / 64];
@@ -202,12 +354,28 @@ __global__ __launch_bounds__(kFeScanThreads) void fe_costscan_kernel(const uint3
     const uint64_t c = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanE;
     uint32_t cur[kScanE];
     if (c + kScanE <= nc) {
-        const uint4 a = *reinterpret_cast<const uint4*>(ccost + c);
-        const uint4 b = *reinterpret_cast<const uint4*>(ccost + c + 4);
+        const uint4 a = *reinterpret_cast<const uint4*>(cfree + c);
+        const uint4 b = *reinterpret_cast<const uint4*>(cfree + c + 4);
         cur[0] = a.x, cur[1] = a.y, cur[2] = a.z, cur[3] = a.w, cur[4] = b.x, cur[5] = b.y, cur[6] = b.z, cur[7] = b.w;
     } else {
 #pragma unroll
-        for (int e = 0; e < kScanE; ++e) cur[e] = c + e < nc ? ccost[c + e] : 0u;
+        for (int e = 0; e < kScanE; ++e) cur[e] = c + e < nc ? cfree[c + e] : 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < kScanE; ++e) {
+        const uint64_t ce = c + e;
+        if (ce >= nc) continue;
+        const uint4 sm = summ[ce];
+        const uint32_t L = sm.y, len = sm.w;
+        const uint32_t ph0 = ce ? (uint32_t)((ce * CH - rsb[ce]) % 255u) : 0u;
+        uint32_t p = ph0, add = 0;
+        if (chunk_starts_run(summ, ce)) {
+            if (ce) add = piece_cost(ph0);
+            p = 0;
+        }
+        add += 5u * ((p + L) / 255u);
+        if (L < len) add += piece_cost((p + L) % 255u);
+        cur[e] += add;
     }
     const uint64_t carry = pass ? tile_carry<false>(agg, blockIdx.x, wt) : 0ull;
     uint64_t ex[kScanE], run = 0;
@@ -228,84 +396,15 @@ __global__ __launch_bounds__(kFeScanThreads) void fe_costscan_kernel(const uint3
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) fc[nc] = all;
 }
 
-// ---- K3: per-byte trigger cost
-__global__ __launch_bounds__(256) void fe_cost_kernel(const uint8_t* __restrict__ x, uint64_t n, uint64_t nc,
-                                                      const uint4* __restrict__ summ, const uint64_t* __restrict__ rsb,
-                                                      uint8_t* __restrict__ cost, uint32_t* __restrict__ ccost) {
-    const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
-    if (c >= nc) return;
-    const int lane = lane_id();
-    const uint64_t c0 = c * CH;
-    const uint32_t len = (uint32_t)min((uint64_t)CH, n - c0);
-    const uint64_t at = c0 + (uint64_t)lane * 64;
-    uint8_t v[64];
-    load64(x, n, at, v);
-    const uint32_t prev_last = __shfl_up((uint32_t)v[63], 1);
-    // byte before the chunk
-    const bool chunk_rs = (c == 0) || ((summ[c].x & 0xff) != ((summ[c - 1].x >> 8) & 0xff));
-    // last run start inside this lane (+1; 0 = none), for the carry scan
-    uint64_t lrs = 0;
-#pragma unroll
-    for (int q = 0; q < 64; ++q) {
-        const uint32_t pos = (uint32_t)lane * 64 + q;
-        const uint32_t prev = q ? v[q - 1] : prev_last;
-        const bool rs = (pos == 0) ? chunk_rs : (pos < len && v[q] != prev);
-        if (rs && pos < len) lrs = c0 + pos + 1;
-    }
-    uint64_t xs = lrs;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t y = __shfl_up(xs, d);
-        if (lane >= d) xs = xs > y ? xs : y;
-    }
-    uint64_t before = __shfl_up(xs, 1);
-    if (lane == 0) before = 0;
-    // run start in effect before this lane's first byte; ph = (i - cur) % 255,
-    // the position of byte i in its run's current 255-byte piece, kept
-    // incrementally (one 64-bit modulo per lane, not per byte)
-    const uint64_t cur = before ? before - 1 : (c == 0 ? 0 : rsb[c]);
-    uint32_t ph = (uint32_t)((at - cur) % 255u);
-    uint32_t sum = 0;
-    uint32_t packed[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) packed[q] = 0;
-#pragma unroll
-    for (int q = 0; q < 64; ++q) {
-        const uint32_t pos = (uint32_t)lane * 64 + q;
-        uint32_t cst = 0;
-        if (pos < len) {
-            const uint32_t prev = q ? v[q - 1] : prev_last;
-            const bool rs = (pos == 0) ? chunk_rs : (v[q] != prev);
-            if (rs) {
-                if (c0 + pos > 0) cst = piece_cost(ph);
-                ph = 0;
-            } else if (ph == 254u) {
-                cst = 5;
-            }
-        }
-        ph = ph == 254u ? 0u : ph + 1u;
-        sum += cst;
-        packed[q >> 2] |= cst << ((q & 3) * 8);
-    }
-    uint4* dst = (uint4*)(cost + at);
-    if (at + 64 <= n) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dst[q] = make_uint4(packed[4 * q], packed[4 * q + 1], packed[4 * q + 2], packed[4 * q + 3]);
-    } else {
-        for (int q = 0; q < 64; ++q)
-            if (at + q < n) cost[at + q] = (uint8_t)(packed[q >> 2] >> ((q & 3) * 8));
-    }
-    sum = wave_sum(sum);
-    if (lane == 0) ccost[c] = sum;
-}
-
 // ---- K5: D map over output positions.  A chunk's entries cover the output
 // range [fc[c], fc[c+1]) exactly once: they are built in LDS by the lanes
 // (64 input bytes each) and written out as one coalesced run.
 constexpr int kDmapMax = CH + CH / 4 + 64;  // RLE1 output of one chunk, at most 5/4 of its bytes
 
-__global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
-                                                      uint64_t n, uint64_t nc, const uint64_t* __restrict__ fc,
-                                                      uint8_t* __restrict__ dmap) {
+__global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict__ x, const uint4* __restrict__ summ,
+                                                      const uint64_t* __restrict__ rsb, uint64_t n, uint64_t nc,
+                                                      const uint64_t* __restrict__ fc, uint8_t* __restrict__ dmap,
+                                                      uint32_t* __restrict__ laneinfo) {
     __shared__ uint8_t stage[4][kDmapMax + 64];  // + one sink byte per lane
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
     if (c >= nc) return;
@@ -313,33 +412,31 @@ __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict_
     const int lane = lane_id();
     const uint64_t c0 = c * CH;
     const uint64_t at = c0 + (uint64_t)lane * 64;
-    // 64 input bytes and their costs as 16 dwords each (plus the next byte / cost)
-    uint32_t xv[17], kv[17];
-    if (at + 68 <= n) {
-        const uint4* px = reinterpret_cast<const uint4*>(x + at);
-        const uint4* pk = reinterpret_cast<const uint4*>(cost + at);
+    // 64 input bytes as 16 dwords (plus the next 4), their costs recomputed
+    // (the per-byte cost array is not materialised)
+    uint32_t xv[17], kv[17], ph0 = 0;
+    {
+        uint32_t w[16];
+        load16w(x, n, at, w);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 a4 = px[q], b4 = pk[q];
-            xv[4 * q] = a4.x; xv[4 * q + 1] = a4.y; xv[4 * q + 2] = a4.z; xv[4 * q + 3] = a4.w;
-            kv[4 * q] = b4.x; kv[4 * q + 1] = b4.y; kv[4 * q + 2] = b4.z; kv[4 * q + 3] = b4.w;
+        for (int q = 0; q < 16; ++q) xv[q] = w[q];
+        uint32_t nx = 0;
+        if (at + 68 <= n) {
+            nx = *reinterpret_cast<const uint32_t*>(x + at + 64);
+        } else {
+            for (int r = 0; r < 4; ++r)
+                if (at + 64 + r < n) nx |= (uint32_t)x[at + 64 + r] << (8 * r);
         }
-        xv[16] = *reinterpret_cast<const uint32_t*>(x + at + 64);
-        kv[16] = *reinterpret_cast<const uint32_t*>(cost + at + 64);
-    } else {
+        xv[16] = nx;
+        const uint32_t len = (uint32_t)min((uint64_t)CH, n - c0);
+        uint32_t pk[16];
+        (void)lane_costs(w, c, len, chunk_starts_run(summ, c), c ? rsb[c] : 0ull, pk, &ph0);
 #pragma unroll
-        for (int q = 0; q < 17; ++q) {
-            uint32_t a1 = 0, b1 = 0;
-            for (int r = 0; r < 4; ++r) {
-                const uint64_t i = at + 4 * q + r;
-                if (i < n) {
-                    a1 |= (uint32_t)x[i] << (8 * r);
-                    b1 |= (uint32_t)cost[i] << (8 * r);
-                }
-            }
-            xv[q] = a1;
-            kv[q] = b1;
-        }
+        for (int q = 0; q < 16; ++q) kv[q] = pk[q];
+        // cost of the byte after the lane: the next lane's first, or the next chunk's
+        uint32_t kn = (uint32_t)__shfl_down((int)(pk[0] & 255u), 1);
+        if (lane == 63) kn = (c + 1 < nc && at + 64 < n) ? chunk_first_cost(summ, rsb, c + 1) : 0u;
+        kv[16] = kn;
     }
     uint32_t lsum = 0;
 #pragma unroll
@@ -349,6 +446,8 @@ __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict_
     }
     const uint32_t incl = wave_incl_sum(lsum);
     uint32_t fl = incl - lsum;  // chunk-local output position
+    // for the chain's in-chunk lookups: the lane's cost prefix and its phase
+    laneinfo[c * 64 + (uint64_t)lane] = fl | (ph0 << 16);
     const uint32_t ctot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     // (entries of the last byte or two of the input stay unwritten: no target
     // reaches them)
@@ -382,32 +481,32 @@ namespace {
 
 struct FeView {
     const uint8_t* x;
-    const uint8_t* cost;
+    const uint32_t* lane;  // per 64-byte lane of a chunk: cost prefix | phase << 16 (fe_dmap_kernel)
     const uint64_t* fc;
     const uint4* summ;
     uint64_t n, nc;
     uint64_t fc_end;  // fc[nc], loaded once
 };
 
-// sum of the cost bytes in [at, at + 64) below `end` (at 16-aligned)
-__device__ __forceinline__ uint32_t cost_sum64(const uint8_t* cost, uint64_t at, uint64_t end) {
-    uint32_t s = 0;
+// cost of byte at + lane of the 64-byte lane window at `at` (whole wave, one
+// byte per lane); ph0 = the piece phase before the window's first byte
+__device__ __forceinline__ uint32_t window_byte_cost(const FeView& f, uint64_t at, uint32_t ph0) {
+    const int lane = lane_id();
+    const uint64_t p = at + (uint64_t)lane;
+    const bool in = p < f.n;
+    const uint32_t b = in ? f.x[p] : 0u, pb = (in && p > 0) ? f.x[p - 1] : 0u;
+    const bool rs = in && (p == 0 || b != pb);
+    uint32_t xs = rs ? (uint32_t)lane + 1u : 0u;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint64_t a = at + 16u * (uint64_t)j;
-        if (a < end) {
-            const uint4 v = *reinterpret_cast<const uint4*>(cost + a);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint64_t b = a + 4u * (uint64_t)q;
-                uint32_t d = w[q];
-                if (b + 4 > end) d = b >= end ? 0u : d & ((1u << (8 * (uint32_t)(end - b))) - 1u);
-                s = __builtin_amdgcn_sad_u8(d, 0u, s);
-            }
-        }
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)xs, d);
+        if (lane >= d) xs = xs > y ? xs : y;
     }
-    return s;
+    uint32_t e = (uint32_t)__shfl_up((int)xs, 1);
+    if (lane == 0) e = 0;
+    const uint32_t ph = e ? ((uint32_t)lane - (e - 1)) % 255u : (ph0 + (uint32_t)lane) % 255u;  // before byte p
+    if (!in) return 0u;
+    return rs ? (p > 0 ? piece_cost(ph) : 0u) : (ph == 254u ? 5u : 0u);
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
@@ -416,18 +515,32 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return (uint64_t)hi << 32 | lo;
 }
 
-// Fg(i) by one wave: chunk prefix + in-chunk sum (all lanes return it)
-__device__ uint64_t fg_at(const FeView& f, uint64_t i) {
+// Fg(i) by one wave: chunk prefix + lane prefix + the window's bytes below i
+// (all lanes return it)
+__device__ __forceinline__ uint64_t fg_at(const FeView& f, uint64_t i) {
     if (i >= f.n) return f.fc_end;
     const uint64_t c = i / CH, c0 = c * CH;
-    const uint32_t s = wave_sum(cost_sum64(f.cost, c0 + 64u * (uint64_t)lane_id(), i));
-    return f.fc[c] + s;
+    const uint32_t L = (uint32_t)((i - c0) >> 6);
+    const uint64_t at = c0 + 64u * L;
+    const uint32_t info = f.lane[c * 64 + L];
+    const uint32_t v = window_byte_cost(f, at, info >> 16);
+    const uint32_t s = wave_sum(at + (uint64_t)lane_id() < i ? v : 0u);
+    return f.fc[c] + (info & 0xffffu) + s;
+}
+
+// cost of byte i (whole wave)
+__device__ __forceinline__ uint32_t byte_cost(const FeView& f, uint64_t i) {
+    const uint64_t c = i / CH, c0 = c * CH;
+    const uint32_t L = (uint32_t)((i - c0) >> 6);
+    const uint64_t at = c0 + 64u * L;
+    const uint32_t v = window_byte_cost(f, at, f.lane[c * 64 + L] >> 16);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(i - at));
 }
 
 // Ginv(y) = min { i : Fg(i) > y } by one wave: a 65-ary search over the
-// chunk prefixes (each lane probes one point per level), lane sums over the
-// chunk, then a scan of the 64 bytes that hold the crossing; n if none.
-__device__ uint64_t ginv(const FeView& f, uint64_t y) {
+// chunk prefixes (each lane probes one point per level), the lane prefixes
+// of the chunk, then a scan of the 64 bytes that hold the crossing; n if none.
+__device__ __forceinline__ uint64_t ginv(const FeView& f, uint64_t y) {
     if (f.fc_end <= y) return f.n;
     const int lane = lane_id();
     uint64_t lo = 0, hi = f.nc;  // fc[lo] <= y < fc[hi]
@@ -439,16 +552,16 @@ __device__ uint64_t ginv(const FeView& f, uint64_t y) {
         lo = nlo;
         hi = nhi;
     }
-    const uint64_t c0 = lo * CH, cend = min(f.n, c0 + CH);
-    const uint64_t at = c0 + 64u * (uint64_t)lane;
-    const uint32_t ls = cost_sum64(f.cost, at, cend);
-    const uint32_t incl = wave_incl_sum(ls);
-    const uint64_t over = __ballot(f.fc[lo] + incl > y);
-    if (!over) return f.n;
-    const int L = __ffsll((long long)over) - 1;
-    const uint64_t baseL = f.fc[lo] + (uint32_t)__builtin_amdgcn_readlane((int)(incl - ls), L);
+    const uint64_t c0 = lo * CH;
+    const uint32_t nl = (uint32_t)((min(f.n, c0 + CH) - c0 + 63) >> 6);  // lanes holding bytes
+    const uint32_t info = (uint32_t)lane < nl ? f.lane[lo * 64 + (uint64_t)lane] : 0xffffffffu;
+    // the crossing lane: the last one whose prefix is <= y (lane 0's is 0)
+    const uint64_t le = __ballot((uint32_t)lane < nl && f.fc[lo] + (info & 0xffffu) <= y);
+    const int L = 63 - __clzll((long long)le);
+    const uint32_t infoL = (uint32_t)__builtin_amdgcn_readlane((int)info, L);
+    const uint64_t baseL = f.fc[lo] + (infoL & 0xffffu);
     const uint64_t atL = c0 + 64u * (uint64_t)L;
-    const uint32_t cb = atL + lane < f.n ? f.cost[atL + lane] : 0u;
+    const uint32_t cb = window_byte_cost(f, atL, infoL >> 16);
     const uint64_t hit = __ballot(baseL + wave_incl_sum(cb) > y);
     return hit ? atL + (uint64_t)__ffsll((long long)hit) : f.n;
 }
@@ -513,13 +626,13 @@ __device__ uint64_t run_end(const FeView& f, uint64_t p) {
 // The chain depends only on the bytes from the entry on (RLE1 state restarts
 // at every block start), so a unit's front end treats its buffer as a stream
 // of its own and the entry comes from the previous unit (bz2mi_shard_chain).
-__global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
+__global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t* __restrict__ x, const uint32_t* __restrict__ laneinfo,
                                                       const uint64_t* __restrict__ fc, const uint4* __restrict__ summ,
                                                       const uint8_t* __restrict__ dmap, uint64_t n, uint64_t nc, int S,
                                                       uint64_t n_own, uint64_t entry, int ends,
                                                       uint64_t* __restrict__ bnd, uint64_t max_bnd,
                                                       uint64_t* __restrict__ nb_out) {
-    FeView f{x, cost, fc, summ, n, nc, uniform64(fc[nc])};
+    FeView f{x, laneinfo, fc, summ, n, nc, uniform64(fc[nc])};
     constexpr uint64_t kExpl = 1ull << 63;
     if (n == 0 || n_own == 0) {
         if (threadIdx.x == 0) {
@@ -530,7 +643,7 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
     }
     // ytot = Fg(n-1): targets y >= ytot have no start inside the buffer;
     // ystop = Fg(n_own-1): targets y >= ystop start at or after n_own
-    const uint64_t ytot = fc[nc] - cost[n - 1];
+    const uint64_t ytot = fc[nc] - byte_cost(f, n - 1);
     const uint64_t ystop = n_own >= n ? ytot : uniform64(fg_at(f, n_own - 1));
     const uint64_t lim = (uint64_t)(S - 6);
     const uint32_t jstar = (uint32_t)((S - 6) / 5 + 1);
@@ -883,12 +996,12 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
 // ---- K7: block ends -> positions: starts[0] = entry, starts[j+1] = the end
 // of block j (bnd[j]); nb_io[2] = the exit token of the next unit
 // (starts[nb] - n_own, bit 63: mid-run), when the unit does not end the stream
-__global__ __launch_bounds__(256) void fe_resolve_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ cost,
+__global__ __launch_bounds__(256) void fe_resolve_kernel(const uint8_t* __restrict__ x, const uint32_t* __restrict__ laneinfo,
                                                          const uint64_t* __restrict__ fc, const uint4* __restrict__ summ,
                                                          uint64_t n, uint64_t nc, uint64_t n_own, uint64_t entry,
                                                          const uint64_t* __restrict__ bnd, uint64_t* __restrict__ nb_io,
                                                          uint64_t* __restrict__ starts) {
-    FeView f{x, cost, fc, summ, n, nc, uniform64(fc[nc])};
+    FeView f{x, laneinfo, fc, summ, n, nc, uniform64(fc[nc])};
     const uint64_t nb = nb_io[0];
     const uint64_t k = (uint64_t)blockIdx.x * 4 + wave_id();
     if (k == 0 && lane_id() == 0) starts[0] = entry & ~(1ull << 63);

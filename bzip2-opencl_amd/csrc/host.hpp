@@ -42,12 +42,13 @@ int dalloc(T** p, size_t count) {
     return BZ2MI_OK;
 }
 
-// Front-end arrays of one byte stream (frontend.hip K1-K7): per-byte costs,
-// the D map, chunk summaries and scans, the block chain and its positions.
+// Front-end arrays of one byte stream (frontend.hip K1-K7): the D map, chunk
+// summaries and scans (d_ccost: the chunks' context-free costs), the block
+// chain and its positions.  Per-byte costs are recomputed where needed.
 struct FrontBufs {
     size_t n_cap = 0, maxb = 0;
-    uint8_t* d_cost = nullptr;
     uint8_t* d_dmap = nullptr;
+    uint32_t* d_lane = nullptr;  // per 64-byte lane: cost prefix | phase << 16
     uint4* d_summ = nullptr;
     uint64_t* d_rsb = nullptr;
     uint32_t* d_ccost = nullptr;
@@ -57,7 +58,7 @@ struct FrontBufs {
     uint64_t* d_nb = nullptr;  // [0] blocks, [1] chain status, [2] exit token
     uint64_t* d_agg = nullptr;  // scan tile aggregates
     std::vector<void*> ptrs() const {
-        return {d_cost, d_dmap, d_summ, d_rsb, d_ccost, d_fc, d_bnd, d_starts, d_nb, d_agg};
+        return {d_dmap, d_lane, d_summ, d_rsb, d_ccost, d_fc, d_bnd, d_starts, d_nb, d_agg};
     }
 };
 

@@ -135,23 +135,26 @@ __global__ void assemble_kernel(const uint32_t* payload, size_t payload_words, c
 
 // Device RLE1 front end (frontend.hip); chunks are 4096 bytes.
 constexpr int kFeChunk = 4096;
-__global__ void fe_summary_kernel(const uint8_t* x, uint64_t n, uint64_t nc, uint4* summ);
+// summ[c] = (first | last byte << 8, lead, trail, len); cfree[c] = the chunk's
+// context-free cost (fe_costscan_kernel adds the incoming run's part)
+__global__ void fe_summary_kernel(const uint8_t* x, uint64_t n, uint64_t nc, uint4* summ, uint32_t* cfree);
 constexpr int kFeScanThreads = 1024;  // threads per scan workgroup
 constexpr int kFeScanTile = kFeScanThreads * 8;  // chunks per scan workgroup
 __global__ void fe_runscan_kernel(const uint4* summ, uint64_t nc, uint64_t* rsb, uint64_t* agg, int pass);
-__global__ void fe_cost_kernel(const uint8_t* x, uint64_t n, uint64_t nc, const uint4* summ, const uint64_t* rsb,
-                               uint8_t* cost, uint32_t* ccost);
-__global__ void fe_costscan_kernel(const uint32_t* ccost, uint64_t nc, uint64_t* fc, uint64_t* agg, int pass);
-__global__ void fe_dmap_kernel(const uint8_t* x, const uint8_t* cost, uint64_t n, uint64_t nc, const uint64_t* fc,
-                               uint8_t* dmap);
+__global__ void fe_costscan_kernel(const uint32_t* cfree, const uint4* summ, const uint64_t* rsb, uint64_t nc,
+                                   uint64_t* fc, uint64_t* agg, int pass);
+// also laneinfo[c*64 + l] = the cost prefix of lane l's 64 bytes in chunk c |
+// their run's piece phase before them << 16 (the chain's in-chunk lookups)
+__global__ void fe_dmap_kernel(const uint8_t* x, const uint4* summ, const uint64_t* rsb, uint64_t n, uint64_t nc,
+                               const uint64_t* fc, uint8_t* dmap, uint32_t* laneinfo);
 constexpr int kFeChainThreads = 1024;  // one workgroup
 // chain of one unit of the stream (own bytes [0, n_own), tail halo up to n),
 // first block at `entry` (bit 63: mid-run); out[0] blocks, out[1] status
-__global__ void fe_chain_kernel(const uint8_t* x, const uint8_t* cost, const uint64_t* fc, const uint4* summ,
+__global__ void fe_chain_kernel(const uint8_t* x, const uint32_t* laneinfo, const uint64_t* fc, const uint4* summ,
                                 const uint8_t* dmap, uint64_t n, uint64_t nc, int S, uint64_t n_own, uint64_t entry,
                                 int ends, uint64_t* bnd, uint64_t max_bnd, uint64_t* out);
 // starts[0..nb] from the chain; nb_io[2] = exit token of the next unit
-__global__ void fe_resolve_kernel(const uint8_t* x, const uint8_t* cost, const uint64_t* fc, const uint4* summ,
+__global__ void fe_resolve_kernel(const uint8_t* x, const uint32_t* laneinfo, const uint64_t* fc, const uint4* summ,
                                   uint64_t n, uint64_t nc, uint64_t n_own, uint64_t entry, const uint64_t* bnd,
                                   uint64_t* nb_io, uint64_t* starts);
 // RLE1 emission + block CRCs (crc_tabs: rle1.hpp crc_device_tables)
