@@ -594,14 +594,31 @@ def bench_e2e(args, ctx, x, n, out, cap):
             os.unlink(src + ".bz2")
             if i >= args.warmup:
                 times.append(dt)
+        # where the time goes (tools/e2e_parts.cpp, same file, page cache warm)
+        parts = None
+        tool = os.path.join(PKG, "build", "e2e_parts")
+        if os.path.exists(tool):
+            r = subprocess.run([tool, src, str(args.level), str(args.parallel), src + ".parts.bz2"], check=True,
+                               capture_output=True, text=True)
+            parts = json.loads(r.stdout)
+            with open(src + ".parts.bz2", "rb") as f:
+                parts["same_bytes"] = hashlib.sha256(f.read()).hexdigest() == want
+        open(os.path.join(d, "empty.bin"), "wb").close()
+        t1 = time.perf_counter()
+        subprocess.run([app, os.path.join(d, "empty.bin"), "-k", "-s", str(args.level), "-p", str(args.parallel)],
+                       check=True, capture_output=True)
+        t_empty = time.perf_counter() - t1
     t = sum(times) / len(times)
+    if parts is not None:
+        parts["app_empty_file_s"] = round(t_empty, 4)  # process start + HIP init + an empty stream + teardown
     line = {"metric": "end-to-end compress MB/s (file -> file, unmodified app.cpp on the mirror headers)",
             "value": round(n / t / 1e6, 2), "unit": "MB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic",
             "config": {"workload": WORKLOADS[args.data].format(mib=args.mib) + " written to a local file",
                        "level": args.level, "parallel_blocks": args.parallel, "unit_bytes": 64 << 20,
-                       "same_bytes_as_device_path": bool(same), "seconds": [round(v, 3) for v in times]}}
+                       "same_bytes_as_device_path": bool(same), "seconds": [round(v, 3) for v in times]},
+            "breakdown": parts}
     print(json.dumps(line), flush=True)
 
 

@@ -1037,12 +1037,15 @@ __device__ __forceinline__ void wave_sort_lds_any(const uint8_t* __restrict__ T,
     }
 }
 
-// `pre`: the batch's SA entries, loaded ahead by the caller (entry e*64+lane in pre[e])
-template <class BL>
-__device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
-                                  const GroupSink& sink, uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
-                                  BL& L, const uint32_t (&pre)[kSmall / 64]) {
-    constexpr int E = kSmall / 64;
+// `pre`: the batch's SA entries, loaded ahead by the caller (entry e*64+lane in
+// pre[e]); E: element slots per lane the batch needs (seg.len <= 64*E), so a
+// random block's batches of ~350 rotations run 6 slots, not kSmall/64 = 8
+template <int E, class BL>
+__device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg,
+                                                    uint32_t d, const GroupSink& sink, uint8_t* __restrict__ bwt,
+                                                    uint32_t* __restrict__ orig, BL& L,
+                                                    const uint32_t (&pre)[kSmall / 64]) {
+    static_assert(E <= kSmall / 64, "slots");
     const int lane = lane_id();
 #pragma unroll
     for (int j = 0; j < 4; ++j) L.base[lane * 4 + j] = 0;
@@ -1217,6 +1220,16 @@ __device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T,
             }
         }
     }
+}
+
+template <class BL>
+__device__ __forceinline__ void wave_sort_bucket2(const uint8_t* __restrict__ T, int n, Scratch& s, Seg seg, uint32_t d,
+                                                  const GroupSink& sink, uint8_t* __restrict__ bwt,
+                                                  uint32_t* __restrict__ orig, BL& L,
+                                                  const uint32_t (&pre)[kSmall / 64]) {
+    if (seg.len <= 384u) wave_sort_bucket2_e<6, BL>(T, n, s, seg, d, sink, bwt, orig, L, pre);
+    else if (seg.len <= 448u) wave_sort_bucket2_e<7, BL>(T, n, s, seg, d, sink, bwt, orig, L, pre);
+    else wave_sort_bucket2_e<8, BL>(T, n, s, seg, d, sink, bwt, orig, L, pre);
 }
 
 // ---- a tie group (<= kTieThread rotations with a common prefix of d

@@ -68,6 +68,7 @@ public:
         }
         sums_.assign(static_cast<size_t>(p_) * 258, 0u);
         carried_.assign(static_cast<size_t>(p_) * 258, 0u);
+        reset();
     }
 
     ~OutputStream()
@@ -78,36 +79,50 @@ public:
     OutputStream(const OutputStream &) = delete;
     OutputStream &operator=(const OutputStream &) = delete;
 
+    // The reference's app.cpp calls this once per input byte (app.cpp:108-114),
+    // so it is one compare and one byte store: the write position is a pointer
+    // bump, and a full buffer (or a closed stream: wend_ == wp_) takes the slow
+    // path.  The position still goes through memory on every call (the byte
+    // store may alias it), so the loop is bound by store-to-load forwarding.
     void write(int value)
     {
-        if (finished_)
-            throw std::runtime_error("Write beyond end of stream");
-        buf_[cur_][fill_++] = static_cast<unsigned char>(value);
-        if (fill_ == cap_)
-            handOver();
+        unsigned char *p = wp_;
+        if (p == wend_)
+        {
+            writeSlow(value);
+            return;
+        }
+        *p = static_cast<unsigned char>(value);
+        wp_ = p + 1;
     }
 
     void write(const std::vector<char> &data, int offset, int length)
     {
         if (finished_)
             throw std::runtime_error("Write beyond end of stream");
+        sync();
         while (length > 0)
         {
+            if (fill_ == cap_)
+                handOver();
             const size_t take = std::min(static_cast<size_t>(length), cap_ - fill_);
             std::memcpy(buf_[cur_] + fill_, data.data() + offset, take);
             fill_ += take;
             offset += static_cast<int>(take);
             length -= static_cast<int>(take);
-            if (fill_ == cap_)
-                handOver();
         }
+        reset();
     }
 
     void close()
     {
         if (finished_)
             return;
+        sync();
+        if (fill_ == cap_)  // a full buffer is handed over as the byte writes left it
+            handOver();
         finished_ = true;
+        reset();
         finishPending();
         if (fill_ > 0)
         {
@@ -147,6 +162,28 @@ private:
         if (ctx_)
             bz2mi_destroy(ctx_);
         ctx_ = nullptr;
+    }
+
+    // fill_ from the write pointer / the write pointer from fill_
+    void sync()
+    {
+        fill_ = static_cast<size_t>(wp_ - buf_[cur_]);
+    }
+    void reset()
+    {
+        wp_ = buf_[cur_] + fill_;
+        wend_ = finished_ ? wp_ : buf_[cur_] + cap_;
+    }
+
+    // write(int) found the buffer full (or the stream closed)
+    void writeSlow(int value)
+    {
+        if (finished_)
+            throw std::runtime_error("Write beyond end of stream");
+        sync();
+        handOver();
+        reset();
+        *wp_++ = static_cast<unsigned char>(value);
     }
 
     static void check(int rc)
@@ -245,6 +282,7 @@ private:
     bz2mi_ctx *ctx_ = nullptr;
     bz2mi_unit *unit_[2] = {nullptr, nullptr};
     unsigned char *buf_[2] = {nullptr, nullptr};
+    unsigned char *wp_ = nullptr, *wend_ = nullptr;  // write position, end of the buffer
     size_t unitBytes_ = 0, halo_ = 0, cap_ = 0, fill_ = 0;
     int cur_ = 0;
     bool finished_ = false, headerDone_ = false;
