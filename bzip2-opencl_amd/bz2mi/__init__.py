@@ -35,6 +35,7 @@ EXPORTS = (
     "bz2mi_dlast_timings", "bz2mi_unit_halo", "bz2mi_unit_create", "bz2mi_unit_destroy", "bz2mi_unit_begin",
     "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode", "bz2mi_unit_assemble", "bz2mi_unit_timings",
     "bz2mi_unit_stats", "bz2mi_host_alloc", "bz2mi_host_free", "bz2mi_unit_begin_host", "bz2mi_unit_assemble_host",
+    "bz2mi_dstream_reset", "bz2mi_dstream",
 )
 
 _lib = None
@@ -90,6 +91,12 @@ def lib() -> ctypes.CDLL:
     L.bz2mi_decompress_device.restype = c.c_int
     L.bz2mi_decompress_device.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
                                           c.POINTER(c.c_size_t), c.c_void_p]
+    if hasattr(L, "bz2mi_dstream"):  # (older A/B builds lack it; test_abi checks the product library)
+        L.bz2mi_dstream_reset.restype = c.c_int
+        L.bz2mi_dstream_reset.argtypes = [c.c_void_p]
+        L.bz2mi_dstream.restype = c.c_int
+        L.bz2mi_dstream.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_uint, c.c_int, c.c_void_p,
+                                    c.c_size_t, c.POINTER(c.c_uint64), c.POINTER(c.c_size_t), c.POINTER(c.c_int)]
     L.bz2mi_dlast_timings.restype = c.c_int
     L.bz2mi_dlast_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
     L.bz2mi_unit_halo.restype = c.c_size_t
@@ -385,6 +392,50 @@ class Decompressor:
         if rc != BZ2MI_OK:
             self._raise(rc)
         return out_len.value
+
+    def stream(self, reader, chunk: int = 16 << 20, window: int = 64 << 20, out_cap: int = 64 << 20):
+        """Streaming decode with bounded memory (bz2mi_dstream): `reader(k)`
+        returns up to k more compressed bytes (b"" at the end); yields the
+        decoded bytes window by window.  Host memory stays O(window + out_cap)."""
+        import numpy as np
+        L = lib()
+        _check(L.bz2mi_dstream_reset(self._h))
+        win = bytearray()
+        bit = 0
+        eof = False
+        out = np.empty(out_cap, dtype=np.uint8)
+        want = window
+        while True:
+            while not eof and len(win) < want:
+                piece = reader(chunk)
+                if not piece:
+                    eof = True
+                else:
+                    win += piece
+            src = np.frombuffer(bytes(win), dtype=np.uint8)
+            end = ctypes.c_uint64(0)
+            n = ctypes.c_size_t(0)
+            fin = ctypes.c_int(0)
+            rc = L.bz2mi_dstream(self._h, src.ctypes.data if src.size else None, src.size, bit, 1 if eof else 0,
+                                 out.ctypes.data, out.size, ctypes.byref(end), ctypes.byref(n), ctypes.byref(fin))
+            if rc == BZ2MI_ESPACE:
+                out = np.empty(n.value + (n.value >> 3) + 4096, dtype=np.uint8)
+                continue
+            if rc != BZ2MI_OK:
+                self._raise(rc)
+            del win[: end.value // 8]
+            bit = end.value & 7
+            if n.value:
+                yield out[: n.value].tobytes()
+                want = window
+            elif fin.value:
+                return
+            elif eof:
+                raise DecompressError("Insufficient data")
+            else:
+                want = len(win) + window
+            if fin.value:
+                return
 
     def timings(self):
         arr = (ctypes.c_float * 6)()

@@ -388,8 +388,10 @@ __device__ __forceinline__ uint32_t long_code(const BitReader& br, const int32_t
     return 0xffffffffu;
 }
 
+// work item j decodes candidate sel[j] (its tables and info) into symbol row j
 __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__ in, uint64_t n,
-                                                     const uint8_t* __restrict__ tabs, uint32_t nids, uint32_t smax,
+                                                     const uint8_t* __restrict__ tabs, const uint32_t* __restrict__ sel,
+                                                     uint32_t nids, uint32_t smax,
                                                      uint16_t* __restrict__ syms, size_t sym_stride,
                                                      DecBlockInfo* __restrict__ infos) {
     // the lookup tables (the table layout's first kTabLimit bytes) of the
@@ -402,17 +404,19 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
     // stage the tables of this wave's blocks
     for (int b = 0; b < kSymBlocks; ++b) {
         if (k0 + b >= nids) break;
-        const uint32_t st = uniform(infos[k0 + b].status);
+        const uint32_t id = uniform(sel[k0 + b]);
+        const uint32_t st = uniform(infos[id].status);
         if (st) continue;
-        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(tabs + (size_t)(k0 + b) * kTabBytes);
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(tabs + (size_t)id * kTabBytes);
         for (int i = lane; i < (int)(kTabLimit / 4); i += 64) tabl[b][i] = s32[i];
     }
     __syncthreads();
     const uint32_t k = k0 + (uint32_t)lane;
     if (lane >= kSymBlocks || k >= nids) return;
-    DecBlockInfo* info = infos + k;
+    const uint32_t id = sel[k];
+    DecBlockInfo* info = infos + id;
     if (info->status) return;
-    const uint8_t* tb = tabs + (size_t)k * kTabBytes;
+    const uint8_t* tb = tabs + (size_t)id * kTabBytes;
     const uint8_t* tl = reinterpret_cast<const uint8_t*>(&tabl[lane][0]);
     const int32_t* lim = reinterpret_cast<const int32_t*>(tb + kTabLimit);
     const int32_t* bas = reinterpret_cast<const int32_t*>(tb + kTabBase);
@@ -522,7 +526,8 @@ __device__ __forceinline__ uint32_t select_zero(uint32_t u, uint32_t k) {
 
 __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict__ syms, size_t sym_stride,
                                                      const uint8_t* __restrict__ symmaps,
-                                                     const uint32_t* __restrict__ blocks, uint32_t nblocks,
+                                                     const uint32_t* __restrict__ blocks,
+                                                     const uint32_t* __restrict__ sym_row, uint32_t nblocks,
                                                      uint32_t smax, uint32_t* __restrict__ scratch, size_t sstride,
                                                      uint8_t* __restrict__ bwt, size_t stride,
                                                      DecBlockInfo* __restrict__ infos) {
@@ -533,9 +538,9 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
     const uint32_t k = uniform(blocks[bi]);
     DecBlockInfo* info = infos + k;
     const uint32_t ns = uniform(info->nsym), eob = uniform(info->alpha) + 1, orig = uniform(info->orig);
-    const uint16_t* so = syms + (size_t)k * sym_stride;
+    const uint16_t* so = syms + (size_t)sym_row[bi] * sym_stride;
     uint32_t* tv = scratch + (size_t)bi * sstride;
-    uint8_t* out = bwt + (size_t)k * stride;
+    uint8_t* out = bwt + (size_t)bi * stride;  // (rows by chain position)
     // chunk [a, b): nominal 64th, start moved past run digits
     uint32_t a = (uint32_t)((uint64_t)ns * (uint32_t)lane / 64u);
     if (lane)
@@ -733,7 +738,7 @@ __device__ __forceinline__ void ibwt_one(IbwtLds& L, uint32_t bi, const uint8_t*
     const int t = threadIdx.x, w = wave_id(), lane = lane_id();
     const uint32_t n = infos[k].len;
     const uint32_t orig = infos[k].orig;
-    const uint8_t* B = bwt + (size_t)k * stride;
+    const uint8_t* B = bwt + (size_t)bi * stride;
     uint32_t* M = merged + (size_t)bi * mstride;
     uint32_t* mark = marks + (size_t)bi * kstride;  // walker id of each start row
     uint8_t* out = rle1 + (size_t)bi * rstride;

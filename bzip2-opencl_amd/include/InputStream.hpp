@@ -3,12 +3,15 @@
 // messages (InputStream.hpp:84,114,121; BlockDecompressor.hpp:111,161,215,248,
 // 276; HuffmanStageDecoder.hpp:55; BitInputStream.hpp:47).
 //
-// Decoding runs on the device (bz2mi_decompress, include/bz2mi.h; SURVEY 8(f)
-// row 1): at the first read the whole input is handed over and every block is
-// decoded at once (Huffman tables, MTF/RLE2, inverse BWT, RLE1 and the block /
-// stream CRCs), then bytes are served from the result.  Errors carry the
-// reference's messages; they surface at the first read() instead of after the
-// bytes of the blocks before the bad one.  As in the reference, blocks are
+// Decoding runs on the device (bz2mi_dstream, include/bz2mi.h; SURVEY 8(f)
+// row 1) in bounded windows: the input is read in kChunk pieces into a window
+// of at least kWindow bytes, every whole block in it is decoded at once
+// (Huffman tables, MTF/RLE2, inverse BWT, RLE1 and the block / stream CRCs),
+// bytes are served from an output buffer of kOutCap bytes, and the window
+// slides on -- host memory stays O(window + output buffer) whatever the input
+// size, as the reference's block-at-a-time reader (InputStream.hpp:51-72).
+// Errors carry the reference's messages and surface after the bytes of the
+// blocks before the failing one.  As in the reference, blocks are
 // limited to digit x 10,000 bytes (Config.hpp:30, BlockDecompressor.hpp:
 // 158-162) and decoding ends at the first end-of-stream marker
 // (InputStream.hpp:136-143).  BZ2MI_BZIP2_COMPAT=1 reads like bzip2 instead:
@@ -20,6 +23,7 @@
 #ifndef INPUT_STREAM_HPP
 #define INPUT_STREAM_HPP
 
+#include <algorithm>
 #include <cstdint>
 #include <istream>
 #include <stdexcept>
@@ -39,11 +43,19 @@ public:
     explicit InputStream(std::istream &in) : in_(in) {}
 
     // next byte, or -1 at the end of the stream
+    ~InputStream()
+    {
+        if (dctx_)
+            bz2mi_ddestroy(dctx_);
+    }
+    InputStream(const InputStream &) = delete;
+    InputStream &operator=(const InputStream &) = delete;
+
     int read()
     {
-        if (pos_ == block_.size() && !refill())
+        if (pos_ == len_ && !refill())
             return -1;
-        return block_[pos_++];
+        return cur_[pos_++];
     }
 
     // up to `length` bytes into buffer[offset..]; -1 at the end of the stream
@@ -52,13 +64,13 @@ public:
         int got = 0;
         while (got < length)
         {
-            if (pos_ == block_.size() && !refill())
+            if (pos_ == len_ && !refill())
                 break;
-            size_t take = block_.size() - pos_;
+            size_t take = len_ - pos_;
             if (take > static_cast<size_t>(length - got))
                 take = static_cast<size_t>(length - got);
             for (size_t i = 0; i < take; ++i)
-                buffer[offset + got + i] = block_[pos_ + i];
+                buffer[offset + got + i] = cur_[pos_ + i];
             pos_ += take;
             got += static_cast<int>(take);
         }
@@ -69,7 +81,13 @@ public:
     {
         done_ = true;
         block_.clear();
-        pos_ = 0;
+        out_.clear();
+        win_.clear();
+        cur_ = nullptr;
+        pos_ = len_ = 0;
+        if (dctx_)
+            bz2mi_ddestroy(dctx_);
+        dctx_ = nullptr;
     }
 
 private:
@@ -109,10 +127,14 @@ private:
             modeChosen_ = true;
             const char *h = std::getenv("BZ2MI_HOST_DECODER");
             host_ = h && *h && *h != '0';
-            if (!host_)
-                return refillDevice();
         }
-        return refillHost();
+        if (!host_)
+            return refillDevice();
+        const bool got = refillHost();
+        cur_ = block_.data();
+        len_ = block_.size();
+        pos_ = 0;
+        return got;
     }
 
     static bool bzip2Compat()
@@ -121,40 +143,84 @@ private:
         return e && *e && *e != '0';
     }
 
-    // the whole input decoded on the device
+    static constexpr size_t kChunk = 16u << 20;    // input read per step
+    static constexpr size_t kWindow = 64u << 20;   // window handed to the device (at least)
+    static constexpr size_t kOutCap = 64u << 20;   // output buffer (grows if one block needs more)
+
+    // the next window's blocks decoded on the device
     bool refillDevice()
     {
-        done_ = true;
-        std::vector<char> in((std::istreambuf_iterator<char>(in_)), std::istreambuf_iterator<char>());
-        int device = 0;
-        if (const char *d = std::getenv("BZ2MI_DEVICE"))
-            device = std::atoi(d);
-        const bool compat = bzip2Compat();
-        bz2mi_dctx *d = bz2mi_dcreate(compat ? BLOCKSIZE_BZIP2 : BLOCKSIZE_DEFAULT, device);
-        if (!d)
-            throw std::runtime_error(std::string("bz2mi: ") + bz2mi_last_error());
-        if (compat)
-            bz2mi_dset_flags(d, BZ2MI_DEC_CONCATENATED);
-        block_.resize(in.size() * 4 + 65536);
-        size_t n = 0;
-        int rc = bz2mi_decompress(d, reinterpret_cast<const uint8_t *>(in.data()), in.size(), block_.data(),
-                                  block_.size(), &n);
-        if (rc == BZ2MI_ESPACE)
+        if (!dctx_)
         {
-            block_.resize(n);
-            rc = bz2mi_decompress(d, reinterpret_cast<const uint8_t *>(in.data()), in.size(), block_.data(),
-                                  block_.size(), &n);
+            int device = 0;
+            if (const char *d = std::getenv("BZ2MI_DEVICE"))
+                device = std::atoi(d);
+            const bool compat = bzip2Compat();
+            dctx_ = bz2mi_dcreate(compat ? BLOCKSIZE_BZIP2 : BLOCKSIZE_DEFAULT, device);
+            if (!dctx_)
+                throw std::runtime_error(std::string("bz2mi: ") + bz2mi_last_error());
+            if (compat)
+                bz2mi_dset_flags(dctx_, BZ2MI_DEC_CONCATENATED);
+            window_ = kWindow;
+            chunk_ = kChunk;
+            size_t outCap = kOutCap;
+            if (const char *w = std::getenv("BZ2MI_DSTREAM_WINDOW"))  // tests: many small windows
+            {
+                window_ = std::max<size_t>(static_cast<size_t>(std::atoll(w)), 64);
+                chunk_ = window_ / 4 + 1;
+                outCap = window_;
+            }
+            out_.resize(outCap);
         }
-        const std::string err = rc == BZ2MI_OK ? std::string() : std::string(bz2mi_last_error());
-        bz2mi_ddestroy(d);
-        if (rc != BZ2MI_OK)
+        size_t want = window_;
+        for (;;)
         {
-            block_.clear();
-            throw std::runtime_error(err);
+            while (!eof_ && win_.size() < want)
+            {
+                const size_t old = win_.size();
+                win_.resize(old + chunk_);
+                in_.read(reinterpret_cast<char *>(win_.data() + old), static_cast<std::streamsize>(chunk_));
+                win_.resize(old + static_cast<size_t>(in_.gcount()));
+                if (!in_)
+                    eof_ = true;
+            }
+            uint64_t end = 0;
+            size_t n = 0;
+            int fin = 0;
+            const int rc = bz2mi_dstream(dctx_, win_.data(), win_.size(), bit_, eof_ ? 1 : 0, out_.data(),
+                                         out_.size(), &end, &n, &fin);
+            if (rc == BZ2MI_ESPACE)
+            {
+                out_.resize(n + (n >> 3) + 4096);
+                continue;
+            }
+            if (rc != BZ2MI_OK)
+            {
+                done_ = true;
+                throw std::runtime_error(bz2mi_last_error());
+            }
+            // slide the window: keep the bytes from the byte holding `end` on
+            const size_t byte = static_cast<size_t>(end / 8);
+            win_.erase(win_.begin(), win_.begin() + static_cast<std::ptrdiff_t>(byte));
+            bit_ = static_cast<unsigned>(end & 7);
+            if (fin)
+                done_ = true;
+            if (n)
+            {
+                cur_ = out_.data();
+                len_ = n;
+                pos_ = 0;
+                return true;
+            }
+            if (fin)
+                return false;
+            if (eof_)  // (a final call decodes something or fails)
+            {
+                done_ = true;
+                throw std::runtime_error("Insufficient data");
+            }
+            want = win_.size() + window_;  // no whole block in the window yet: a longer one
         }
-        block_.resize(n);
-        pos_ = 0;
-        return !block_.empty();
     }
 
     bool refillHost()
@@ -386,8 +452,15 @@ private:
     bool host_ = false;
     int maxBlock_ = 0;
     uint32_t streamCRC_ = 0;
-    std::vector<uint8_t> block_;
-    size_t pos_ = 0;
+    std::vector<uint8_t> block_;           // host decoder: the current block
+    bz2mi_dctx *dctx_ = nullptr;            // device decoder
+    std::vector<uint8_t> win_;              // device decoder: the input window
+    std::vector<uint8_t> out_;              // device decoder: decoded bytes
+    unsigned bit_ = 0;                      // window bit where decoding resumes
+    size_t window_ = 0, chunk_ = 0;
+    bool eof_ = false;                      // the input is read to its end
+    const uint8_t *cur_ = nullptr;          // bytes being served
+    size_t len_ = 0, pos_ = 0;
 };
 
 #endif

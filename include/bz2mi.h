@@ -195,8 +195,11 @@ int bz2mi_unit_stats(bz2mi_unit* u, uint64_t* out4);
 /* ---- decompression on the device ----------
  * Replaces the reference's InputStream (InputStream.hpp:36-159),
  * BlockDecompressor (BlockDecompressor.hpp:37-282) and HuffmanStageDecoder
- * (HuffmanStageDecoder.hpp:30-136): every block of the stream is decoded at
- * once.  Errors are BZ2MI_EFORMAT with the reference's message ("Invalid BZip2
+ * (HuffmanStageDecoder.hpp:30-136): the blocks of the stream are decoded
+ * together, as many at once as a memory budget allows (max(64 x the input,
+ * 1 GiB) of per-block device buffers, BZ2MI_DEC_BUDGET overrides: a
+ * legitimate stream is one window, an input of crafted magic matches is
+ * decoded a bounded number of candidates at a time).  Errors are BZ2MI_EFORMAT with the reference's message ("Invalid BZip2
  * header", "BZip2 block CRC error", "BZip2 stream CRC error", "BZip2 stream
  * format error", "block Huffman tables invalid", "Error decoding  block",
  * "BZip2 block exceeds declared block size", "BZip2 start pointer invalid",
@@ -222,6 +225,25 @@ int bz2mi_decompress(bz2mi_dctx* d, const uint8_t* in, size_t n, uint8_t* out, s
 /* device buffers (HBM); hip_stream: hipStream_t or NULL (the context's) */
 int bz2mi_decompress_device(bz2mi_dctx* d, const void* d_in, size_t n, void* d_out, size_t cap, size_t* out_len,
                             void* hip_stream);
+
+/* Streaming decode with bounded memory (the reference's block-at-a-time
+ * InputStream, InputStream.hpp:51-72,125-158).  in[0, n) is a window of the
+ * compressed input and decoding resumes at window bit `start_bit`; every block
+ * that lies whole inside the window is decoded, at most `cap` output bytes and
+ * a bounded number of blocks per call (device memory of the decoded
+ * candidates <= BZ2MI_DSTREAM_BUDGET bytes, default 1 GiB).  *end_bit: the
+ * window bit where the next call resumes (the caller keeps the bytes from
+ * *end_bit / 8 on and appends more input); *done = 1 once the stream (or, with
+ * BZ2MI_DEC_CONCATENATED, the streams) ended.  *out_len = 0 with *done = 0:
+ * the window holds no whole block yet -- hand over a longer one (final = 0)
+ * or, with final = 1 (no more input), the call reports "Insufficient data".
+ * An error is returned by the call after the one that returned the bytes of
+ * the blocks before the failing one, as the reference throws when it reaches
+ * that block.  BZ2MI_ESPACE: *out_len = the bytes the next block needs.
+ * bz2mi_dstream_reset starts a new input. */
+int bz2mi_dstream_reset(bz2mi_dctx* d);
+int bz2mi_dstream(bz2mi_dctx* d, const uint8_t* in, size_t n, unsigned start_bit, int final, uint8_t* out,
+                  size_t cap, uint64_t* end_bit, size_t* out_len, int* done);
 
 /* milliseconds of the last call: [0] candidate scan, [1] Huffman symbols,
  * [2] MTF + RLE2 (and the stream walk), [3] inverse BWT, [4] RLE1 + CRC, [5] whole call */

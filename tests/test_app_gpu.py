@@ -88,3 +88,29 @@ def test_app_round_trip_with_its_decoder(tmp_path):
     assert (tmp_path / "x.bin").read_bytes() == data
     r = subprocess.run([APP, str(p), "-c"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "Integrity check passed" in r.stdout
+
+
+def test_app_decodes_in_small_windows(tmp_path):
+    """The mirror InputStream decodes in bounded windows (bz2mi_dstream): with
+    windows of 200 KB a multi-block file decodes to the same bytes, and a
+    corrupted one fails with the reference's message."""
+    from bz2mi import synth
+    data = synth.mixed_bytes(3 << 20, segment=256 << 10).tobytes()
+    src = tmp_path / "w.bin"
+    src.write_bytes(data)
+    r = subprocess.run([APP, str(src), "-k", "-s", "9", "-p", "10"], capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    z = tmp_path / "w.bin.bz2"
+    src.unlink()
+    env = dict(os.environ, BZ2MI_DSTREAM_WINDOW="200000")
+    r = subprocess.run([APP, str(z), "-d", "-k"], capture_output=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert src.read_bytes() == data
+    r = subprocess.run([APP, str(z), "-c"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "Integrity check passed" in r.stdout, (r.stdout, r.stderr)
+    bad = bytearray(z.read_bytes())
+    bad[len(bad) // 2] ^= 0x08
+    zb = tmp_path / "bad.bin.bz2"
+    zb.write_bytes(bytes(bad))
+    r = subprocess.run([APP, str(zb), "-c"], capture_output=True, text=True, env=env, timeout=300)
+    assert "error" in (r.stdout + r.stderr).lower() or r.returncode != 0, (r.stdout, r.stderr)

@@ -137,3 +137,87 @@ def test_full_size_round_trip_on_device(bz):
         got = d.decompress_device(z.data_ptr(), zn, y.data_ptr(), n)
     assert got == n
     assert torch.equal(x, y)
+
+
+# ---- streaming decode with bounded memory (bz2mi_dstream; the reference's
+# block-at-a-time InputStream, InputStream.hpp:51-72,125-158)
+
+def _reader(z: bytes):
+    pos = [0]
+
+    def read(k):
+        piece = z[pos[0]: pos[0] + k]
+        pos[0] += len(piece)
+        return piece
+    return read
+
+
+@pytest.mark.parametrize("level", [9, 1])
+def test_stream_decode_small_windows(bz, dec, level):
+    """Windows far smaller than the stream (blocks cut by window ends, blocks
+    that need a longer window, output buffers that hold a few blocks and
+    grow when one block needs more) give the whole-input bytes."""
+    from bz2mi import synth
+    for name, data in [("mixed", synth.mixed_bytes(5 << 20, segment=300 << 10).tobytes()),
+                       ("runs_long", synth.runs_bytes(2 << 20, max_run=5000).tobytes()),
+                       ("one", b"x"), ("empty", b"")]:
+        z = bz.compress(data, level, 10)
+        for chunk, window, cap in [(37_000, 150_000, 300_000), (5_000, 20_000, 50_000), (1 << 20, 4 << 20, 8 << 20)]:
+            got = b"".join(dec.stream(_reader(z), chunk=chunk, window=window, out_cap=cap))
+            assert got == data, (name, level, chunk, window, cap)
+
+
+def test_stream_decode_golden_and_concatenated(bz, manifest):
+    with bz.Decompressor(10000) as d:
+        for name, e in sorted(manifest["cases"].items()):
+            data = golden_input(name)
+            for st in e["streams"]:
+                z = golden_file(st["file"])
+                assert b"".join(d.stream(_reader(z), chunk=4096, window=16384, out_cap=1 << 16)) == data, name
+    a, b = b"first stream " * 5000, b"second" * 7000
+    z = bz2.compress(a, 9) + bz2.compress(b, 9) + b"trailing junk"
+    with bz.Decompressor(100000, concatenated=True) as d:
+        assert b"".join(d.stream(_reader(z), chunk=3000, window=9000, out_cap=1 << 16)) == a + b
+    with bz.Decompressor(100000) as d:  # the reference: the first stream only
+        assert b"".join(d.stream(_reader(z), chunk=3000, window=9000, out_cap=1 << 16)) == a
+
+
+def test_stream_decode_error_after_the_good_blocks(bz, dec):
+    """A corrupted block in the middle: the blocks before it come out, then the
+    reference's message (the same the whole-input call reports)."""
+    from bz2mi import synth
+    data = synth.random_bytes(3 << 20).tobytes()   # ~35 blocks of 90,000 bytes
+    z = bytearray(bz.compress(data, 9, 10))
+    z[len(z) // 2] ^= 0x10
+    z = bytes(z)
+    with pytest.raises(bz.DecompressError) as whole:
+        dec.decompress(z)
+    got = []
+    with pytest.raises(bz.DecompressError) as streamed:
+        for piece in dec.stream(_reader(z), chunk=100_000, window=400_000, out_cap=1 << 20):
+            got.append(piece)
+    got = b"".join(got)
+    assert str(streamed.value) == str(whole.value)
+    assert len(got) > (1 << 20) and data.startswith(got)
+
+
+def test_crafted_magics_allocate_bounded_memory(bz):
+    """16 MiB of block magics after a stream header: the decoder reports the
+    reference's error, and its device memory stays within a few times the
+    input (the input's device copy, the candidate list, the table budget)
+    instead of growing with the number of matches (~2.8 M here)."""
+    import torch
+    n = 16 << 20
+    z = b"BZh9" + b"1AY&SY" * (n // 6)
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    with bz.Decompressor(10000) as d:
+        with pytest.raises(bz.DecompressError):
+            d.decompress(z, cap=1 << 20)
+        free1, _ = torch.cuda.mem_get_info()
+        with pytest.raises(bz.DecompressError):
+            for _ in d.stream(_reader(z), chunk=4 << 20, window=8 << 20, out_cap=1 << 20):
+                pass
+        free2, _ = torch.cuda.mem_get_info()
+    used = free0 - min(free1, free2)
+    assert used <= 4 * len(z) + (32 << 20), used
