@@ -17,8 +17,11 @@ compresses its units with the unit protocol of include/bz2mi.h:
                 (entry, first block index) per unit, passed in stream order;
                 a rank's blocks start compressing as soon as its chain is done
                 while the token travels on;
-  2. sums    -- all-gather of the per-unit slot sums (p x 258 uint32); the
-                carried seeds of unit g are the sum over the units before it;
+  2. sums    -- the running sum of the per-unit slot sums (p x 258 uint32)
+                passed in stream order like the chain token: the carried
+                seeds of unit g are the sum over the units before it, and a
+                unit is encoded (Huffman) as soon as they arrive, overlapping
+                the later units' BWT / MTF;
   3. encode  -- all-gather of (bits, CRC share, blocks) per unit; exclusive scan
                 of the bits gives each unit's stream bit offset, the CRC shares
                 combine as crc' = rotl(crc, m) ^ share;
@@ -136,28 +139,53 @@ def compress_units(units: dict, owners: list[int], parallel: int, level: int, gr
         if g + 1 < total and owners[g + 1] != me:
             exs = ex - (1 << 64) if ex >= (1 << 63) else ex  # int64 bit pattern
             dist.send(torch.tensor([exs, first + nb], dtype=torch.int64), dst=owners[g + 1], group=group, tag=g + 1)
+    # 2. slot sums -> carried seeds, passed in stream order like the chain
+    # token (unit g's seeds are the uint32 sum of the slot sums of every unit
+    # before it): a unit is encoded as soon as its own sums and the running
+    # sum are known, so its Huffman coding overlaps the later units' BWT / MTF
+    # instead of waiting for every unit of the stream
+    w = parallel * 258
+    acc = None
+    rows = np.zeros((len(mine), 3), dtype=np.int64)
+    local = _group_size(group) == 1
+    if local:  # one rank: offsets are known unit by unit too, so it assembles as it goes
+        wb_all = [g for g in range(total) if nblocks_local[g] > 0]
+        first_u = wb_all[0] if wb_all else -1
+        last_u = wb_all[-1] if wb_all else -1
+        G = C = 0
+        offs_l = [-1] * total
+        crcb_l = [0] * total
+        pieces = {}
+    for i, g in enumerate(mine):
+        if g == 0:
+            acc = np.zeros(w, dtype=np.uint32)
+        elif owners[g - 1] != me:
+            t = torch.zeros(w, dtype=torch.int32)
+            dist.recv(t, src=owners[g - 1], group=group, tag=total + 1 + g)
+            acc = t.numpy().view(np.uint32).copy()
+        carried = acc.copy()
+        acc = acc + units[g].sums().astype(np.uint32)   # uint32 wrap-around, as the reference's int array
+        if g + 1 < total and owners[g + 1] != me:
+            dist.send(torch.from_numpy(acc.view(np.int32).copy()), dst=owners[g + 1], group=group, tag=total + 2 + g)
+        bits, crc = units[g].encode(carried)
+        rows[i] = (bits, crc & 0xFFFFFFFF, nblocks_local[g])
+        if local and nblocks_local[g] > 0:
+            offs_l[g], crcb_l[g] = G, C
+            flags = (UNIT_FIRST if g == first_u else 0) | (UNIT_LAST if g == last_u else 0)
+            pieces[g] = units[g].assemble(G, C, flags)
+            G += bits + (32 if g == first_u else 0)
+            C = _rotl(C, nblocks_local[g]) ^ (crc & 0xFFFFFFFF)
+    if local:
+        nbl = [nblocks_local[g] for g in range(total)]
+        bl = [int(rows[i][0]) for i in range(total)]
+        if first_u < 0:
+            return Layout(nbl, bl, [-1] * total, [0] * total, -1, -1, 14 * 8, 0, list(owners), empty=True)
+        lay = Layout(nbl, bl, offs_l, crcb_l, first_u, last_u, G + 80, C, list(owners))
+        lay.pieces = pieces
+        return lay
+    # 3. encode results -> bits, CRC share, blocks
     counts = [sum(1 for o in owners if o == r) for r in range(_group_size(group))]
     by_rank = [[g for g in range(total) if owners[g] == r] for r in range(len(counts))]
-    # 2. slot sums -> carried seeds
-    w = parallel * 258
-    rows = np.zeros((len(mine), w), dtype=np.int64)
-    for i, g in enumerate(mine):
-        rows[i] = units[g].sums().astype(np.int64)
-    tabs = _all_gather_rows(rows, counts, group)
-    sums = np.zeros((total, w), dtype=np.uint32)
-    for r, tab in enumerate(tabs):
-        for i, g in enumerate(by_rank[r]):
-            sums[g] = tab[i].astype(np.uint32)
-    carried = np.zeros((total, w), dtype=np.uint32)
-    acc = np.zeros(w, dtype=np.uint32)
-    for g in range(total):
-        carried[g] = acc
-        acc = acc + sums[g]   # uint32 wrap-around, as the reference's int array
-    # 3. encode -> bits, CRC share, blocks
-    rows = np.zeros((len(mine), 3), dtype=np.int64)
-    for i, g in enumerate(mine):
-        bits, crc = units[g].encode(carried[g])
-        rows[i] = (bits, crc, nblocks_local[g])
     tabs = _all_gather_rows(rows, counts, group)
     nbl = [0] * total
     bl = [0] * total

@@ -53,11 +53,19 @@ struct bz2mi_unit {
     size_t own_cap = 0;
     uint8_t* d_out = nullptr;  // host-fed units: assembled bytes
     size_t out_cap = 0;
+    uint8_t* h_pin = nullptr;  // pinned staging of the carried seeds and the encode results (async copies)
 };
 
 namespace {
 
 bool stage_ok(bz2mi_unit* u, int want) { return u && u->stage >= want; }
+
+// word copy by a kernel, between device and pinned host memory: the unit's
+// small control copies stay on its stream's queue (a DMA-engine copy there
+// measured as waiting for work queued on the other streams)
+__global__ void copy_words_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
 
 }  // namespace
 
@@ -105,6 +113,7 @@ void bz2mi_unit_destroy(bz2mi_unit* u) {
     if (u->d_state) (void)hipFree(u->d_state);
     if (u->d_sd) (void)hipFree(u->d_sd);
     if (u->d_vol) (void)hipFree(u->d_vol);
+    if (u->h_pin) (void)hipHostFree(u->h_pin);
     if (u->ev_in) (void)hipEventDestroy(u->ev_in);
     for (auto& e : u->ev)
         if (e) (void)hipEventDestroy(e);
@@ -175,10 +184,12 @@ int bz2mi_unit_chain(bz2mi_unit* u, uint64_t entry, uint64_t first_block, uint64
     if ((r = stage_mtf(c, t, cnt, c->sM))) return r;
     HIPCHECK(hipEventRecord(u->ev[5], c->sM));
     HIPCHECK(hipEventRecord(t.evM, c->sM));
-    HIPCHECK(hipStreamWaitEvent(c->sB, t.evM, 0));
-    HIPCHECK(hipMemsetAsync(u->d_state, 0, sizeof(uint32_t) * c->p * bz2mi::kMaxAlpha, c->sB));
-    if ((r = stage_seed(c, t, cnt, first_block, u->d_state, c->sB))) return r;
-    HIPCHECK(hipEventRecord(u->ev[6], c->sB));
+    // this unit's slot sums right behind its MTF on stream M: stream B stays
+    // free for the Huffman coding of units whose seeds are known (a wait for
+    // a later unit's MTF queued on B would hold the earlier units' coding back)
+    HIPCHECK(hipMemsetAsync(u->d_state, 0, sizeof(uint32_t) * c->p * bz2mi::kMaxAlpha, c->sM));
+    if ((r = stage_seed(c, t, cnt, first_block, u->d_state, c->sM))) return r;
+    HIPCHECK(hipEventRecord(u->ev[6], c->sM));
     u->stage = 2;
     return BZ2MI_OK;
 }
@@ -214,8 +225,20 @@ int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, ui
     Batch& t = u->t;
     hipStream_t s = c->sB;
     const size_t ne = (size_t)c->p * bz2mi::kMaxAlpha;
-    // seeds: the carried sums of the earlier units, then this unit's running sums
-    HIPCHECK(hipMemcpyAsync(u->d_state, carried, ne * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    // seeds: the carried sums of the earlier units, then this unit's running
+    // sums (after its MTF and its own slot sums on stream M)
+    // (bz2mi_unit_sums has normally waited for it on the host already; a
+    // device-side wait on an event of stream M measured as a wait for
+    // everything queued on M later -- the Huffman coding of unit 0 started
+    // after the last unit's MTF -- so the stream waits only if it must)
+    if (hipEventQuery(u->ev[6]) != hipSuccess) HIPCHECK(hipStreamWaitEvent(s, u->ev[6], 0));
+    // pinned staging: a copy from pageable memory is carried out synchronously
+    // behind the device's other queued work (measured: unit 0's coding waited
+    // for the last unit's MTF)
+    if (!u->h_pin) HIPCHECK(hipHostMalloc((void**)&u->h_pin, ne * sizeof(uint32_t) + 256, hipHostMallocDefault));
+    std::memcpy(u->h_pin, carried, ne * sizeof(uint32_t));
+    hipLaunchKernelGGL(copy_words_kernel, dim3(4), dim3(256), 0, s, reinterpret_cast<const uint32_t*>(u->h_pin),
+                       u->d_state, (int)ne);
     HIPCHECK(hipEventRecord(u->ev[7], s));
     if ((r = stage_seed(c, t, cnt, u->first_block, u->d_state, s))) return r;
     if ((r = stage_huffman(c, t, cnt, s))) return r;
@@ -228,9 +251,16 @@ int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, ui
     HIPCHECK(hipGetLastError());
     bz2mi::StreamDev sd{};
     uint64_t total = 0;
-    HIPCHECK(hipMemcpyAsync(&total, t.d_offs + cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipMemcpyAsync(&sd, u->d_sd, sizeof(sd), hipMemcpyDeviceToHost, s));
+    uint8_t* res = u->h_pin + ne * sizeof(uint32_t);  // (its bytes after the seeds: 256 >= 8 + sizeof(sd))
+    static_assert(sizeof(bz2mi::StreamDev) + 8 <= 256, "pinned result area");
+    hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const uint32_t*>(t.d_offs + cnt),
+                       reinterpret_cast<uint32_t*>(res), 2);
+    hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const uint32_t*>(u->d_sd),
+                       reinterpret_cast<uint32_t*>(res + 8), (int)(sizeof(sd) / 4));
+    HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(s));
+    std::memcpy(&total, res, sizeof(uint64_t));
+    std::memcpy(&sd, res + 8, sizeof(sd));
     u->bits = total;
     u->crc = sd.crc;
     *bits = total;
