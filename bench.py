@@ -51,7 +51,7 @@ def ensure_built():
         subprocess.run(["make", "-C", PKG, "-j8"], check=True, stdout=subprocess.DEVNULL)
 
 
-TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r02_traffic_{data}.json")
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r03_traffic_{data}.json")
 
 
 def stage_traffic(args, stage):

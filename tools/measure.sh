@@ -8,11 +8,13 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${TAG:-r2r}
 mkdir -p $O
 prof() {  # $1 = data, $2 = extra bench args
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_$1 -o run -- python3 $R/bench.py --data $1 --no-cpu $2 > $O/stats_$1.log 2>&1 || { echo STATS_$1_FAILED; tail $O/stats_$1.log; exit 1; }
-  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$1 -o run -- python3 $R/bench.py --data $1 --no-cpu --no-verify --steps 1 --warmup 1 > $O/pmc_fetch_$1.log 2>&1 || { echo FETCH_$1_FAILED; exit 1; }
-  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$1 -o run -- python3 $R/bench.py --data $1 --no-cpu --no-verify --steps 1 --warmup 1 > $O/pmc_write_$1.log 2>&1 || { echo WRITE_$1_FAILED; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_$1 -o run -- python3 $R/bench.py --data $1 --no-cpu --no-900k $2 > $O/stats_$1.log 2>&1 || { echo STATS_$1_FAILED; tail $O/stats_$1.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$1 -o run -- python3 $R/bench.py --data $1 --no-cpu --no-900k --no-verify --steps 1 --warmup 1 > $O/pmc_fetch_$1.log 2>&1 || { echo FETCH_$1_FAILED; exit 1; }
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$1 -o run -- python3 $R/bench.py --data $1 --no-cpu --no-900k --no-verify --steps 1 --warmup 1 > $O/pmc_write_$1.log 2>&1 || { echo WRITE_$1_FAILED; exit 1; }
 }
-if [ "${PART:-A}" = A ]; then
+if [ "${PART:-A}" = R ]; then
+  prof random ""
+elif [ "${PART:-A}" = A ]; then
   timeout -k 10 900 python -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS_FAILED; grep -E "FAIL|Error" $O/tests.log | head; tail -30 $O/tests.log; exit 1; }
   tail -3 $O/tests.log
   timeout -k 10 300 python3 $R/bench.py > $O/bench.json 2> $O/bench.err || { echo BENCH_FAILED; tail $O/bench.err; exit 1; }

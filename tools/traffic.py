@@ -22,7 +22,7 @@ for counter, sub, scale in (("FETCH_SIZE", "pmc_fetch", 2.0), ("WRITE_SIZE", "pm
     for r in csv.DictReader(open(f"{src}/{sub}{suffix}/run_counter_collection.csv")):
         if "bz2mi::" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
             continue
-        k = r["Kernel_Name"].split("(")[0].replace("bz2mi::", "")
+        k = r["Kernel_Name"].split("(")[0].replace("bz2mi::", "").replace("void ", "")
         key = "fetch_bytes" if counter == "FETCH_SIZE" else "write_bytes"
         per[k][key] += float(r["Counter_Value"]) * 1024.0 * scale / steps
         if counter == "FETCH_SIZE":
