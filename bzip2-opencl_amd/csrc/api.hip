@@ -644,10 +644,17 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
         const size_t bits = 24 + 272 + 18 + (S / 50 + 1) * 6 + 6 * (5 + 258 * 39) + (S + 1) * 20;
         c->payload_words = (bits + 31) / 32 + 4;
     }
+    // stream B (seeds, Huffman, assembly) at the highest priority: when the
+    // stages of several batches / stream units are in flight, the kernels that
+    // finish a unit are dispatched ahead of the MTF / BWT kernels of later ones
+    // (at equal priority the hardware queues served those first and the
+    // units' Huffman kernels formed a tail)
+    int prio_lo = 0, prio_hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->sA, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->sM, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->sB, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->sB, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithFlags(&c->sF, hipStreamNonBlocking) != hipSuccess) {
         fail(BZ2MI_EDEVICE, "hipStreamCreate failed");
         bz2mi_destroy(c);
