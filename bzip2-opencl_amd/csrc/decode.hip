@@ -456,15 +456,13 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
             }
         }
         br.skip((int)len);
-        if (br.pos > br.nbits) {
-            status = kDecData;
-            break;
-        }
+        // (reading past the end is checked once, after the loop: the reader
+        // returns zero bits there, and a block that ran past the end fails
+        // with kDecData whatever it decoded meanwhile)
         push(sym);
         if ((++ns & 7u) == 0) *reinterpret_cast<uint4*>(so + ns - 8) = make_uint4(a0, a1, a2, a3);
-        if (sym == eob) break;
-        if (ns >= ns_max) {
-            status = kDecSize;
+        if (sym == eob || ns >= ns_max) {
+            if (sym != eob) status = kDecSize;
             break;
         }
         if (--gleft == 0) {  // next group of 50 (HuffmanStageDecoder.hpp:50-57)
@@ -477,6 +475,7 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
             gleft = kGroupRun;
         }
     }
+    if (br.pos > br.nbits) status = kDecData;
     if (ns & 7u) {  // the last partial 8 (zeros after it: the stride is a multiple of 64 symbols)
         for (uint32_t q = ns & 7u; q < 8; ++q) push(0u);
         *reinterpret_cast<uint4*>(so + (ns & ~7u)) = make_uint4(a0, a1, a2, a3);
