@@ -124,6 +124,15 @@ struct BitReader {
         pos += k;
         refill();
     }
+    // skip without keeping `pos` (the symbol loop): position() recovers it
+    // from the reader state -- bits loaded up to word wnext minus the unread
+    // ones (pf, res, buf)
+    __device__ __forceinline__ void skip_fast(int k) {  // k <= 32
+        buf <<= k;
+        nb -= k;
+        refill();
+    }
+    __device__ __forceinline__ uint64_t position() const { return wnext * 32 - 64 - (uint64_t)rb - (uint64_t)nb; }
     __device__ __forceinline__ void check() {
         if (pos > nbits) over = true;
     }
@@ -455,7 +464,7 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
                 break;
             }
         }
-        br.skip((int)len);
+        br.skip_fast((int)len);
         // (reading past the end is checked once, after the loop: the reader
         // returns zero bits there, and a block that ran past the end fails
         // with kDecData whatever it decoded meanwhile)
@@ -475,6 +484,7 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
             gleft = kGroupRun;
         }
     }
+    br.pos = br.position();
     if (br.pos > br.nbits) status = kDecData;
     if (ns & 7u) {  // the last partial 8 (zeros after it: the stride is a multiple of 64 symbols)
         for (uint32_t q = ns & 7u; q < 8; ++q) push(0u);
