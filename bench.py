@@ -52,6 +52,15 @@ def ensure_built():
 
 
 TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r03_traffic_{data}.json")
+# the kernels of each timed stage (bz2mi_compress_device, csrc/api.hip)
+STAGE_KERNELS = {
+    "front": "fe_summary/runscan/costscan/dmap/chain/resolve (scans + block chain) and fe_rle1_kernel",
+    "bwt": "bwt_block_kernel x2 (mode 0: first-byte scatter + batch sorts; mode 1: blocks the text kernel hands "
+           "back), bwt_text_kernel, bwt_wlevel/level/block_small kernels, bwt_tie_kernel x6, bwt_double_kernel",
+    "mtf": "mtf_kernel<G>",
+    "huffman": "huffman_kernel",
+    "assemble": "offsets_dev_kernel, assemble_dev_kernel, advance_kernel",
+}
 
 
 def stage_traffic(args, stage):
@@ -308,6 +317,10 @@ def main():
     roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
             "algorithmic_bytes": int(alg[dom]), "avg_ms": round(avg[dom], 3),
+            "stage_kernels": STAGE_KERNELS.get(dom),
+            "what": "HIP events around the stage's launches on the stream they run on, per step; the stage is "
+                    "the kernels listed (their rocprofv3 durations sum to avg_ms: profiles/r03_kernel_stats_"
+                    + args.data + "_v2.csv)",
             "pipeline_GBps": round((n + out_len) / (ms_step * 1e-3) / 1e9, 2),
             "stage_ms": {k: round(v, 3) for k, v in avg.items()}}
     # the metric's literal wording, "900KB blocks": the same input at -9 in the
