@@ -40,6 +40,10 @@ WORKLOADS = {
               "one .bz2 stream per GPU",
     "text": "C3: {mib} MiB seeded word-Markov text per GPU (synth.text_bytes, seed 0x5EED0002+rank; enwik9 "
             "stand-in) resident in HBM -> one .bz2 stream per GPU",
+    "realtext": "C3: {mib} MiB enwik9-like text per GPU (synth.realtext_bytes, seed 0x5EED0004+rank: mixed case, "
+                "digits, MediaWiki/XML markup and page headers, UTF-8 words, repeated 0.2-20 KB passages; ~150 "
+                "distinct bytes per 90 KB block; enwik9 itself is not available offline) resident in HBM -> one .bz2 "
+                "stream per GPU",
     "mixed": "C4: {mib} MiB mixed-entropy stream per GPU (synth.mixed_bytes, seed 0x5EED0003+rank, 64 MiB "
              "segments of random/text/runs/ACGT) resident in HBM -> one .bz2 stream per GPU",
 }
@@ -208,9 +212,10 @@ def main():
                     help="compress = the bench line (BASELINE metric); decompress = configs[4]: device "
                          "decompression of the stream this run compresses (output MB/s); e2e = file -> file "
                          "through the reference's unmodified app.cpp built against the mirror headers")
-    ap.add_argument("--data", choices=["random", "text", "mixed"], default="random",
-                    help="random = C2 (the bench line); text = C3 stand-in (seeded word Markov text, enwik9 is "
-                         "not available offline); mixed = C4 (rotating random/text/runs/ACGT segments)")
+    ap.add_argument("--data", choices=["random", "text", "realtext", "mixed"], default="random",
+                    help="random = C2 (the bench line); realtext = C3 stand-in (enwik9-like: ~150 distinct bytes "
+                         "per block, markup, UTF-8, long repeats; enwik9 is not available offline); text = 27-symbol "
+                         "word Markov text; mixed = C4 (rotating random/text/runs/ACGT segments)")
     ap.add_argument("--units-per-gpu", type=int, default=None,
                     help="units of the logical stream per rank (interleaved over the ranks); N > 1 default 4; "
                          "given at N = 1, the unit protocol runs on the one device (the base of a 1 -> N curve)")
@@ -253,8 +258,13 @@ def main():
         x = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
     else:
         from bz2mi import synth
-        gen = synth.text_bytes if args.data == "text" else synth.mixed_bytes
-        x = torch.from_numpy(gen(n, (synth.SEED_TEXT if args.data == "text" else synth.SEED_MIXED) + rank)).to(dev)
+        if args.data == "realtext":
+            host = synth.realtext_bytes(n, synth.SEED_REALTEXT + rank, threads=host_cpu()["cores_used_parallel"])
+        else:
+            gen = synth.text_bytes if args.data == "text" else synth.mixed_bytes
+            host = gen(n, (synth.SEED_TEXT if args.data == "text" else synth.SEED_MIXED) + rank)
+        x = torch.from_numpy(host).to(dev)
+        del host
     cap = bz2mi.compress_bound(n, args.level, args.unit)
     out = torch.empty(cap, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -389,6 +399,8 @@ def unit_bytes(args, g: int, U: int, dev):
         return torch.randint(0, 256, (U,), dtype=torch.uint8, device=dev, generator=gen)
     if args.data == "text":
         return torch.from_numpy(synth.text_bytes(U, synth.SEED_TEXT + g)).to(dev)
+    if args.data == "realtext":
+        return torch.from_numpy(synth.realtext_bytes(U, synth.SEED_REALTEXT + g, threads=8)).to(dev)
     seg = 64 << 20
     assert U % seg == 0, "mixed units are whole 64 MiB segments"
     return torch.from_numpy(synth.mixed_bytes(U, synth.SEED_MIXED, seg, first_segment=g * (U // seg))).to(dev)
@@ -572,7 +584,8 @@ def bench_units(args, world: int):
 
 
 WORKLOAD_DATA = {"random": "random bytes, unit g seeded 0x5EED0001+g", "text": "word-Markov text, unit g seeded "
-                 "0x5EED0002+g", "mixed": "C4 mixed-entropy segments, seed 0x5EED0003"}
+                 "0x5EED0002+g", "realtext": "enwik9-like text, unit g seeded 0x5EED0004+g",
+                 "mixed": "C4 mixed-entropy segments, seed 0x5EED0003"}
 
 
 def bench_e2e(args, ctx, x, n, out, cap):

@@ -168,7 +168,8 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         for (int mode = 0; mode < 2; ++mode) {
             if (mode == 1 && text_path) {
                 hipLaunchKernelGGL(bwt_text_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
-                                   t.d_sa, t.d_bwt, t.d_orig, t.d_present, t.d_redo, c->d_lspill, t.d_groups);
+                                   t.d_sa, t.d_bwt, t.d_orig, t.d_redo, c->d_lspill, t.d_groups, c->d_tq[0],
+                                   c->d_tq[1], tcap);
                 HIPCHECK(hipGetLastError());
             }
             if (mode == 1 && !text_path) {  // every text-like block back to the general path

@@ -1775,10 +1775,11 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
 constexpr int FT = 1024;
 constexpr int FW = FT / 64;
 
-// Text-like blocks (at most kTextAlpha distinct bytes) are deferred by mode 0
-// to bwt_text_kernel (redo[b] = 1), which hands back the ones it cannot finish
-// (redo[b] = 2: periodic or very long repeats, a full work queue) to mode 1.
-constexpr int kTextAlpha = 64;    // distinct bytes of a text-path block
+// Text-like blocks (at least half of the rotations in first-byte buckets of
+// more than kSmall) are deferred by mode 0 to bwt_text_kernel (redo[b] = 1),
+// which hands back the ones it cannot finish (redo[b] = 2: periodic blocks, a
+// full work queue or pair list) to mode 1.  Random-like blocks (buckets of
+// ~n/256) stay on this path.
 constexpr int kTextMinN = 4096;   // smaller blocks stay on this path
 
 // Pair path of bwt_block_kernel: up to kPair of a block's largest first-byte
@@ -1854,8 +1855,9 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     if (t < 256) sh.base[t] = ex;
     if (mode == 0) {
         // text-like blocks: the symbol map, then bwt_text_kernel
-        const int K = __syncthreads_count(c != 0u);
-        if (K <= kTextAlpha && n >= kTextMinN) {
+        uint32_t bigsum;
+        (void)wg_excl_sum<FT>(c > (uint32_t)kSmall ? c : 0u, L.tmp, &bigsum);
+        if (2 * bigsum >= (uint32_t)n && n >= kTextMinN) {
             if (t < 256) {
                 const uint64_t m = __ballot(c != 0);
                 if (lane_id() == 0) {
@@ -2337,50 +2339,96 @@ __global__ __launch_bounds__(FT) void bwt_block_small_kernel(const uint8_t* __re
     }
 }
 
-// ---- kernel 1t: text-like blocks (at most kTextAlpha distinct bytes), one
-// 1024-thread workgroup per block with the block's text in LDS.  Induced
-// sorting in the manner of bzip2's main sort (Seward's "copy" step):
-//   * every rotation is scattered into its two-byte bucket (a, b);
+// ---- kernel 1t: text-like blocks (most rotations in first-byte buckets of
+// more than kSmall), one 1024-thread workgroup per block with the block's
+// text in LDS.  Induced sorting in the manner of bzip2's main sort (Seward's
+// "copy" step):
+//   * every rotation is scattered into its two-byte bucket (a, b): a counting
+//     sort by the first byte, then every first-byte row split by the second
+//     byte (one wave per row, largest rows first).  The non-empty pair buckets
+//     form a sparse index: a 256-bit mask of second bytes per first byte and
+//     the row's entries in a list, so any alphabet (up to 256 bytes, ~2,000
+//     non-empty pairs in a 90 KB block of real text) fits;
 //   * the first-byte buckets are processed in ascending size; for bucket ss
 //     every pair bucket (ss, b) whose b is not yet processed (and (ss, ss)) is
 //     sorted -- partitions by the next byte and wave sorts, all keys read from
-//     the LDS text, work spread over the 16 waves through an LDS work queue --
-//     while the pair buckets (ss, b) of processed b are already in order;
+//     the LDS text, work spread over the 16 waves -- while the pair buckets
+//     (ss, b) of processed b are already in order;
 //   * then bucket ss is complete, and for every unprocessed x the pair bucket
 //     (x, ss) follows for free: the rotations i-1 of the sorted bucket ss with
 //     T[i-1] = x, in that order (a stable partition by the preceding byte).
 // About half of the rotations of text are placed by the copy step without
 // being sorted.  BWT bytes and origPtr are written as positions become final.
-// Blocks it cannot finish (ties deeper than kTextDcap bytes: periodic blocks,
-// very long repeats; a full work queue) get redo[b] = 2 and go through the
-// general path (bwt_block_kernel mode 1).
-constexpr int kTextDcap = 512;   // depth at which a tie or a partition gives up
-
-constexpr int kTextChain = 32;    // levels a partition goes down with one child before the block is handed back
-constexpr int kTQ = 512;
-constexpr int kCopyR = 4;        // rotations per lane and chunk of a copy step         // work items per round
-constexpr int kTW = 768;         // per-wave LDS words
+// Long repeats: rotations still tied after kTextTieCap bytes are not sorted
+// further.  Their SA entries are flagged (kUnres: the run holds the right set
+// of rotations, in an unknown order), the copy steps carry the flag to the
+// rotations they place from them, and after the copy steps the flagged runs
+// are ordered by prefix doubling (Larsson-Sadakane with a depth per group):
+// a group whose rotations share h bytes is sorted on the rank of rotation
+// i + h, where a final rotation's rank is its position and a flagged one's the
+// first position of its group (with the group's depth).  Blocks it cannot
+// finish (periodic blocks, a group larger than kSmall, a full work queue or
+// pair list) get redo[b] = 2 and go through the general path
+// (bwt_block_kernel mode 1).
+constexpr int kTextDcap = 512;    // depth at which a partition gives up
+constexpr int kTextChain = 32;    // levels a partition goes down with one child before its segment is deferred
+#ifndef BZ2MI_TEXT_TIECAP
+#define BZ2MI_TEXT_TIECAP 64
+#endif
+constexpr int kTextTieCap = BZ2MI_TEXT_TIECAP;  // tie depth after which a wave sort defers its tied groups
+#ifndef BZ2MI_TEXT_PAIRCAP
+#define BZ2MI_TEXT_PAIRCAP 256
+#endif
+constexpr int kTextPairCap = BZ2MI_TEXT_PAIRCAP;  // depth to which two tied rotations are compared directly
+constexpr int kTQ = 512;          // work items per round
+constexpr int kCopyR = 4;         // rotations per lane and chunk of a copy step
+constexpr int kTW = 768;          // per-wave LDS words
+constexpr uint32_t kUnres = 0x80000000u;  // SA entry flag: a deferred (unordered) run
+constexpr int kResolveIters = 48;  // doubling rounds before a block is handed back (periodic blocks)
+constexpr uint32_t kDepthMax = 0x7fffu;
+// non-empty (first, second byte) pairs of a text-path block (~2,000 in a 90 KB
+// block of real text): counted in the per-wave scratch during the setup, and
+// the pair list (uint64 entries) lives in the block's group area, which holds
+// stride / 2 of them (more than kPairCap at every level with S >= 20,000)
+constexpr int kPairCap = FW * kTW - FW * 256 - 1;  // the copy steps keep the starts in LDS beside 16 x 256 cursors
+// copy-processed first-byte buckets (the largest ones); the smaller buckets are
+// sorted whole and copied from in one step
+#ifndef BZ2MI_TEXT_COPYSTEPS
+#define BZ2MI_TEXT_COPYSTEPS 24
+#endif
+constexpr int kCopySteps = BZ2MI_TEXT_COPYSTEPS;
 
 struct TextLds {
     uint4 text[kBwtLdsText / 16];
-    union {
-        uint32_t cur[kTextAlpha * kTextAlpha];  // pair-bucket cursors (the scatter)
-        uint32_t w[FW][kTW];                    // per-wave scratch (the steps)
-    } u;
+    uint32_t w[FW][kTW];              // per-wave scratch
     uint64_t q[2][kTQ];               // work items of this round / the next: depth | len | start
-    uint32_t pcol[kTextAlpha];        // start of (x, ss) for the copy targets
-    uint32_t cstart[kTextAlpha + 1];  // first-byte bucket starts
+    uint32_t mask[256][8];            // pair index: second bytes present, per first byte
+    uint32_t rowoff[256];             // a first byte's first entry in the pair list
+    uint32_t pcol[256];               // start of (x, ss) for the copy targets
+    uint32_t cstart[257];             // first-byte bucket starts
     uint32_t tmp[FW];
-    uint32_t qn[2], fail;
-    uint8_t id[256];                  // byte -> dense id
-    uint8_t order[kTextAlpha];        // ids by ascending bucket size
-    uint8_t rank[kTextAlpha];         // position of an id in that order
-    uint8_t target[kTextAlpha];
-    uint8_t own[kTextAlpha * kTextAlpha];  // the wave that sorts a pair bucket / a round's item
+    uint32_t wlo[FW], whi[FW];        // a wave's range of pair entries (the deal)
+    uint32_t qn[2], fail, nflag;
+    uint8_t order[256];               // bytes by ascending bucket size
+    uint8_t rank[256];                // position of a byte in that order
+    uint8_t target[256];
+    uint8_t own[kTQ];                 // the wave of a round's item
 #ifdef BZ2MI_PHASES
     uint32_t stat[16];
 #endif
 };
+static_assert(sizeof(TextLds) <= 160 * 1024, "text kernel LDS");
+
+// Pair-list entry: start (17) | len (17) | second byte (8) | first byte (8) |
+// sorted explicitly (1) | owner wave (4)
+__device__ __forceinline__ uint64_t pe_make(uint32_t start, uint32_t len, uint32_t b, uint32_t a, bool expl) {
+    return (uint64_t)start | ((uint64_t)len << 17) | ((uint64_t)b << 34) | ((uint64_t)a << 42) |
+           ((uint64_t)(expl ? 1u : 0u) << 50);
+}
+__device__ __forceinline__ uint32_t pe_start(uint64_t e) { return (uint32_t)e & 0x1ffffu; }
+__device__ __forceinline__ uint32_t pe_len(uint64_t e) { return (uint32_t)(e >> 17) & 0x1ffffu; }
+__device__ __forceinline__ bool pe_expl(uint64_t e) { return (e >> 50) & 1u; }
+__device__ __forceinline__ uint32_t pe_owner(uint64_t e) { return (uint32_t)(e >> 51) & 15u; }
 
 // SA / spill words the text kernel reads back after this wave or another of
 // the workgroup rewrote them: plain loads.  The waves of a workgroup share the
@@ -2408,18 +2456,6 @@ __device__ __forceinline__ void tq_push(TextLds& L, int nxt, bool want, uint32_t
         if (pos < (uint32_t)kTQ) L.q[nxt][pos] = tq_item(start, len, depth);
         else atomicOr(&L.fail, 1u);
     }
-}
-
-// match of a 6-bit value over the valid lanes
-__device__ __forceinline__ uint64_t wave_match6(uint32_t key, bool valid) {
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-        const bool bit = (key >> b) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-    }
-    return peers;
 }
 
 // TBK_TRACE builds: every wave's last position in the text kernel, stored to
@@ -2483,8 +2519,84 @@ __device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t po
     if (i == 0) *orig = pos;
 }
 
+// Tied items of a wave sort (W[0, tt): index | slot << 17 | group head << 26,
+// groups in slot order) at depth D: every group of exactly two rotations is
+// ordered by comparing the LDS text directly, 8 bytes at a time, up to
+// kTextPairCap bytes (one lane per pair; the repeats of text tie in pairs),
+// or flagged (kUnres) when they still tie there; the items of larger groups
+// are compacted to W[0, return) for another tie round.
+__device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_t* sa, uint32_t base, uint32_t tt,
+                                               uint32_t D, uint8_t* out, uint32_t* orig, uint32_t* W, TextLds& L) {
+    constexpr int E = kSmall / 64;
+    const int lane = lane_id();
+    uint32_t wv[E];
+    bool keep[E], ph[E];
+    uint32_t nkeep = 0, nfl = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t q = (uint32_t)(lane * E + e);
+        wv[e] = q < tt ? W[q] : 0u;
+        const bool h0 = q < tt && (wv[e] >> 26);
+        const bool h1 = q + 1 < tt && (W[q + 1] >> 26);
+        const bool h2 = q + 2 >= tt || (W[q + 2] >> 26);
+        ph[e] = h0 && q + 1 < tt && !h1 && h2;  // the head of a group of two
+        const bool hm = q >= 1 && (W[q - 1] >> 26) && !h0 && (q + 1 >= tt || h1);  // its second item
+        keep[e] = q < tt && !ph[e] && !hm;
+        nkeep += keep[e] ? 1u : 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (!ph[e]) continue;
+        const uint32_t q = (uint32_t)(lane * E + e);
+        const uint32_t w1 = W[q + 1];
+        const uint32_t i0 = wv[e] & 0x1ffffu, i1 = w1 & 0x1ffffu;
+        const uint32_t s0 = (wv[e] >> 17) & 511u, s1 = (w1 >> 17) & 511u;
+        const uint32_t lo = min(s0, s1);
+        uint32_t p0 = (i0 + D) % (uint32_t)n, p1 = (i1 + D) % (uint32_t)n;
+        int cmp = 0;
+        for (uint32_t dd = D; dd < (uint32_t)kTextPairCap; dd += 8) {
+            const uint64_t x0 = load8(Tl, n, p0), x1 = load8(Tl, n, p1);
+            if (x0 != x1) {
+                cmp = x0 < x1 ? -1 : 1;
+                break;
+            }
+            p0 += 8;
+            p1 += 8;
+            if (p0 >= (uint32_t)n) p0 -= (uint32_t)n;
+            if (p1 >= (uint32_t)n) p1 -= (uint32_t)n;
+        }
+        if (cmp) {
+            const uint32_t a = cmp < 0 ? i0 : i1, c = cmp < 0 ? i1 : i0;
+            sa[base + lo] = a;
+            sa[base + lo + 1] = c;
+            text_final(Tl, n, base + lo, a, out, orig);
+            text_final(Tl, n, base + lo + 1, c, out, orig);
+        } else {
+            sa[base + lo] = i0 | kUnres;
+            sa[base + lo + 1] = i1 | kUnres;
+            nfl += 2;
+        }
+    }
+    const uint32_t nf = wave_sum(nfl);
+    if (nf && lane == 0) atomicAdd(&L.nflag, nf);
+    const uint32_t inc = wave_incl_sum(nkeep);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    __builtin_amdgcn_wave_barrier();  // every lane has read W before it is compacted
+    if (tot != tt) {
+        uint32_t o = inc - nkeep;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (keep[e]) W[o++] = wv[e];
+        __builtin_amdgcn_wave_barrier();
+    }
+    return tot;
+}
+
 // sort a segment of <= kSmall rotations with a common prefix of d bytes (one
-// wave; keys from the LDS text); final SA entries, BWT bytes, origPtr
+// wave; keys from the LDS text); final SA entries, BWT bytes, origPtr.  Items
+// still tied after kTextTieCap bytes keep their slots with the kUnres flag
+// (ordered by the resolve pass).
 #ifndef TBK_SORT_INL
 #define TBK_SORT_INL __forceinline__
 #endif
@@ -2515,10 +2627,20 @@ __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, S
     TBK_COUNT(7, seg.len);
     uint32_t D = d + kLdsKeyBytes;
     while (tt) {
+        tt = uniform(text_pairs(Tl, n, sa, seg.start, tt, D, out, orig, W, L));
+        if (!tt) break;
         TBK_T(8, D << 12 | tt);
         TBK_COUNT(10, 1);
-        if (D + kLdsTieBytes > (uint32_t)kTextDcap) {
-            if (lane == 0) atomicOr(&L.fail, 1u);
+        if (D + kLdsTieBytes > (uint32_t)kTextTieCap) {
+            // deferred: the tied items keep their slots, flagged
+            for (uint32_t q0 = 0; q0 < tt; q0 += 64) {
+                const uint32_t q = q0 + (uint32_t)lane;
+                if (q < tt) {
+                    const uint32_t w = W[q];
+                    sa[seg.start + ((w >> 17) & 511u)] = (w & 0x1ffffu) | kUnres;
+                }
+            }
+            if (lane == 0) atomicAdd(&L.nflag, tt);
             return;
         }
         tt = uniform(lds_tie_round_any(Tl, n, s, seg.start, tt, D, out, orig, W));
@@ -2528,7 +2650,9 @@ __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, S
 
 // partition a segment of > kSmall rotations with a common prefix of d bytes
 // by byte d (one wave): children of one rotation are final, runs of small
-// ones go to the queue as batches, large ones as items of depth d+1
+// ones go to the queue as batches, large ones as items of depth d+1.  A
+// segment that is still one child kTextChain levels down (or at kTextDcap) is
+// deferred whole (flagged).
 __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* spill, Seg seg, uint32_t d,
                                uint8_t* out, uint32_t* orig, uint32_t* W, TextLds& L, int nxt) {
     const int lane = lane_id();
@@ -2541,7 +2665,8 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     const uint32_t dcap = min((uint32_t)kTextDcap, d + (uint32_t)kTextChain);
     for (;;) {
         if (d >= dcap) {
-            if (lane == 0) atomicOr(&L.fail, 1u);
+            for (uint32_t k = lane; k < seg.len; k += 64) sa[seg.start + k] = ld_fresh(sa + seg.start + k) | kUnres;
+            if (lane == 0) atomicAdd(&L.nflag, seg.len);
             return;
         }
         TBK_COUNT(5, 1);
@@ -2636,12 +2761,263 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     __builtin_amdgcn_wave_barrier();
 }
 
+// common prefix length of rotations i and j, capped at `cap` (a multiple of 8)
+__device__ __forceinline__ uint32_t text_lcp(const uint8_t* Tl, int n, uint32_t i, uint32_t j, uint32_t cap) {
+    uint32_t l = 0;
+    uint32_t pi = i, pj = j;
+    while (l < cap) {
+        const uint64_t x = load8(Tl, n, pi) ^ load8(Tl, n, pj);
+        if (x) return l + ((uint32_t)__builtin_clzll(x) >> 3);
+        l += 8;
+        pi += 8;
+        pj += 8;
+        if (pi >= (uint32_t)n) pi -= (uint32_t)n;
+        if (pj >= (uint32_t)n) pj -= (uint32_t)n;
+    }
+    return cap;
+}
+
+// Rank word of a rotation during the resolve: position << 15 | depth, where
+// a final rotation has its own position and depth 0 and a flagged one the
+// first position of its group and the group's depth (a lower bound of the
+// common prefix of its rotations, >= 2).  Sorting rank words sorts by
+// position.
+__device__ __forceinline__ uint32_t rw_make(uint32_t pos, uint32_t depth) { return (pos << 15) | depth; }
+
+// resolve: one group of 3..kSmall rotations at `head` sorted by its keys (one wave)
+template <int E>
+__device__ __forceinline__ void resolve_wave(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa,
+                                             const uint32_t* key, uint8_t* out, uint32_t* orig, uint32_t head,
+                                             uint32_t m, uint32_t depth, uint32_t* W, TextLds& L, uint32_t* gnext,
+                                             int nxt) {
+    const int lane = lane_id();
+    uint64_t k[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(e * 64 + lane);
+        k[e] = g < m ? ((uint64_t)ld_fresh(key + head + g) << 32) | (ld_fresh(sa + head + g) & 0x1ffffu) : ~0ull;
+    }
+    uint32_t dummy[E];
+    wave_bitonic<E, false>(k, dummy);
+    // sorted: item r = lane * E + e
+    const uint32_t pk = lane_prev((uint32_t)(k[E - 1] >> 32), 0u);
+    bool hd[E];
+    uint32_t run = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t r = (uint32_t)lane * E + e;
+        const uint32_t kw = (uint32_t)(k[e] >> 32);
+        const uint32_t prev = e ? (uint32_t)(k[e - 1] >> 32) : pk;
+        hd[e] = r < m && (r == 0 || kw != prev);
+        if (hd[e]) run = r;
+        if (r < m) W[r] = hd[e] ? 1u : 0u;
+    }
+    if (lane == 0) W[m] = 1u;
+    const uint32_t carry = lane_prev(wave_incl_max(run), 0u);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t cur = carry;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t r = (uint32_t)lane * E + e;
+        if (hd[e]) cur = r;
+        bool want = false;
+        uint32_t glen = 0;
+        if (r < m) {
+            const uint32_t i = (uint32_t)k[e] & 0x1ffffu, kw = (uint32_t)(k[e] >> 32);
+            const uint32_t pos = head + r;
+            const bool single = hd[e] && W[r + 1];
+            if (single) {
+                sa[pos] = i;
+                isa[i] = rw_make(pos, 0);
+                text_final(Tl, n, pos, i, out, orig);
+            } else {
+                const uint32_t nd = min(depth + (kw & kDepthMax), kDepthMax);
+                sa[pos] = i | kUnres;
+                isa[i] = rw_make(head + cur, nd);
+                if (hd[e]) {
+                    glen = 1;
+                    while (!W[r + glen]) ++glen;
+                    want = true;
+                }
+            }
+        }
+        const uint64_t mm = __ballot(want);
+        if (mm) {
+            uint32_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&L.qn[nxt], (uint32_t)__popcll(mm));
+            b0 = uniform(b0);
+            if (want) gnext[b0 + (uint32_t)__popcll(mm & __lanemask_lt())] = (head + r) | ((glen - 1) << 17);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Order the flagged runs (the whole workgroup, after the copy steps): groups
+// are the flagged runs split where the first two bytes change, each with the
+// common prefix of its rotations (min of neighbour LCPs, capped); then rounds
+// of doubling until no group is left.  isa: n words, key: n words, glist:
+// two lists of n/2 + 1 words.  Returns false when the block has to go back.
+__device__ void text_resolve(const uint8_t* Tl, int n, uint32_t* __restrict__ sa, uint32_t* __restrict__ isa,
+                             uint32_t* __restrict__ key, uint32_t* __restrict__ glist, uint8_t* __restrict__ out,
+                             uint32_t* orig, TextLds& L) {
+    const int t = threadIdx.x, w = wave_id();
+    uint32_t* W = L.w[w];
+    uint32_t* gl[2] = {glist, glist + ((uint32_t)n / 2 + 1)};
+    if (t == 0) L.qn[0] = 0;
+    __syncthreads();
+    for (uint32_t k = t; k < (uint32_t)n; k += FT) {
+        const uint32_t v = ld_fresh(sa + k), i = v & 0x1ffffu;
+        if (!(v & kUnres)) {
+            isa[i] = rw_make(k, 0);
+            continue;
+        }
+        const uint32_t pi = ((uint32_t)Tl[i] << 8) | Tl[i + 1 < (uint32_t)n ? i + 1 : 0u];
+        bool head = k == 0;
+        if (!head) {
+            const uint32_t u = ld_fresh(sa + k - 1), iu = u & 0x1ffffu;
+            head = !(u & kUnres) || (((uint32_t)Tl[iu] << 8) | Tl[iu + 1 < (uint32_t)n ? iu + 1 : 0u]) != pi;
+        }
+        if (!head) continue;
+        uint32_t len = 1, dep = (uint32_t)kTextPairCap & ~7u, prev = i;
+        while (k + len < (uint32_t)n) {
+            const uint32_t u = ld_fresh(sa + k + len), iu = u & 0x1ffffu;
+            if (!(u & kUnres) || (((uint32_t)Tl[iu] << 8) | Tl[iu + 1 < (uint32_t)n ? iu + 1 : 0u]) != pi) break;
+            dep = min(dep, text_lcp(Tl, n, prev, iu, dep));
+            prev = iu;
+            if (++len > (uint32_t)kSmall) break;
+        }
+        if (len > (uint32_t)kSmall) {
+            atomicOr(&L.fail, 1u);
+            continue;
+        }
+        if (len == 1) {
+            sa[k] = i;
+            isa[i] = rw_make(k, 0);
+            text_final(Tl, n, k, i, out, orig);
+            continue;
+        }
+        dep = max(dep, 2u);
+        for (uint32_t j = 0; j < len; ++j) isa[ld_fresh(sa + k + j) & 0x1ffffu] = rw_make(k, dep);
+        gl[0][atomicAdd(&L.qn[0], 1u)] = k | ((len - 1) << 17);
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int it = 0, cur = 0;; ++it, cur ^= 1) {
+        const uint32_t ng = uniform(L.qn[cur]);
+        if (ng == 0 || uniform(L.fail)) break;
+        if (it >= kResolveIters) {
+            if (t == 0) L.fail = 1u;
+            break;
+        }
+        __syncthreads();  // every thread has read the count
+        if (t == 0) L.qn[cur ^ 1] = 0;
+        const uint32_t* ga = gl[cur];
+        // keys: the rank word of rotation i + depth, for every member (a
+        // snapshot).  Groups of two (nearly all: repeats tie in pairs) U at a
+        // time per thread with their loads in flight together; larger groups
+        // one member at a time.
+        constexpr int U = 4;
+        for (uint32_t g0 = t; g0 < ng; g0 += FT * U) {
+            uint32_t e[U], v0[U], v1[U], dp[U], k0[U], k1[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t g = g0 + (uint32_t)u * FT;
+                e[u] = g < ng ? ga[g] : 0xffffffffu;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t head = e[u] & 0x1ffffu;
+                v0[u] = e[u] != 0xffffffffu ? sa[head] & 0x1ffffu : 0u;
+                v1[u] = e[u] != 0xffffffffu ? sa[head + 1] & 0x1ffffu : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) dp[u] = e[u] != 0xffffffffu ? isa[v0[u]] & kDepthMax : 0u;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                k0[u] = e[u] != 0xffffffffu ? isa[(v0[u] + dp[u]) % (uint32_t)n] : 0u;
+                k1[u] = e[u] != 0xffffffffu ? isa[(v1[u] + dp[u]) % (uint32_t)n] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (e[u] == 0xffffffffu) continue;
+                const uint32_t head = e[u] & 0x1ffffu, len = (e[u] >> 17) + 1;
+                key[head] = k0[u];
+                key[head + 1] = k1[u];
+                for (uint32_t j = 2; j < len; ++j)
+                    key[head + j] = isa[((sa[head + j] & 0x1ffffu) + dp[u]) % (uint32_t)n];
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+        // pairs: one thread each, U at a time
+        for (uint32_t g0 = t; g0 < ng; g0 += FT * U) {
+            uint32_t e[U], v0[U], v1[U], k0[U], k1[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t g = g0 + (uint32_t)u * FT;
+                const uint32_t x = g < ng ? ga[g] : 0xffffffffu;
+                e[u] = (x != 0xffffffffu && (x >> 17) == 1u) ? x : 0xffffffffu;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t head = e[u] & 0x1ffffu;
+                const bool ok = e[u] != 0xffffffffu;
+                v0[u] = ok ? sa[head] & 0x1ffffu : 0u;
+                v1[u] = ok ? sa[head + 1] & 0x1ffffu : 0u;
+                k0[u] = ok ? key[head] : 0u;
+                k1[u] = ok ? key[head + 1] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (e[u] == 0xffffffffu) continue;
+                const uint32_t head = e[u] & 0x1ffffu;
+                const uint32_t i0 = v0[u], i1 = v1[u];
+                if (k0[u] == k1[u]) {
+                    const uint32_t dep = isa[i0] & kDepthMax;
+                    const uint32_t nd = min(dep + (k0[u] & kDepthMax), kDepthMax);
+                    isa[i0] = rw_make(head, nd);
+                    isa[i1] = rw_make(head, nd);
+                    gl[cur ^ 1][atomicAdd(&L.qn[cur ^ 1], 1u)] = e[u];
+                } else {
+                    const bool sw = k1[u] < k0[u];
+                    const uint32_t a = sw ? i1 : i0, c = sw ? i0 : i1;
+                    sa[head] = a;
+                    sa[head + 1] = c;
+                    isa[a] = rw_make(head, 0);
+                    isa[c] = rw_make(head + 1, 0);
+                    text_final(Tl, n, head, a, out, orig);
+                    text_final(Tl, n, head + 1, c, out, orig);
+                }
+            }
+        }
+        // larger groups: one wave each (chunks of 64 list entries dealt to the waves)
+        for (uint32_t g0 = (uint32_t)w * 64; g0 < ng; g0 += FT) {
+            const uint32_t g = g0 + (uint32_t)lane_id();
+            const uint32_t e = g < ng ? ld_fresh(ga + g) : 0u;
+            const uint32_t len = (e >> 17) + 1;
+            for (uint64_t mm = __ballot(g < ng && len > 2); mm; mm &= mm - 1) {
+                const int l = __builtin_ctzll(mm);
+                const uint32_t ee = uniform((uint32_t)__shfl((int)e, l));
+                const uint32_t head = ee & 0x1ffffu, m = (ee >> 17) + 1;
+                const uint32_t dep = uniform(ld_fresh(isa + (ld_fresh(sa + head) & 0x1ffffu)) & kDepthMax);
+                if (m <= 64) resolve_wave<1>(Tl, n, sa, isa, key, out, orig, head, m, dep, W, L, gl[cur ^ 1], cur ^ 1);
+                else if (m <= 128) resolve_wave<2>(Tl, n, sa, isa, key, out, orig, head, m, dep, W, L, gl[cur ^ 1], cur ^ 1);
+                else if (m <= 256) resolve_wave<4>(Tl, n, sa, isa, key, out, orig, head, m, dep, W, L, gl[cur ^ 1], cur ^ 1);
+                else resolve_wave<8>(Tl, n, sa, isa, key, out, orig, head, m, dep, W, L, gl[cur ^ 1], cur ^ 1);
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict__ blocks, size_t stride,
                                                       const uint32_t* __restrict__ lens, int nblocks,
                                                       uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
-                                                      uint32_t* __restrict__ orig_out,
-                                                      const uint32_t* __restrict__ present, uint32_t* __restrict__ redo,
-                                                      uint32_t* __restrict__ spill_all, Seg* __restrict__ grp_all) {
+                                                      uint32_t* __restrict__ orig_out, uint32_t* __restrict__ redo,
+                                                      uint32_t* __restrict__ spill_all, Seg* __restrict__ grp_all,
+                                                      uint64_t* __restrict__ key_all, uint64_t* __restrict__ glist_all,
+                                                      size_t tcap) {
     __shared__ TextLds L;
     const int b = blockIdx.x;
     if (b >= nblocks || redo[b] != 1u) return;
@@ -2656,147 +3032,184 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     uint32_t* orig = orig_out + b;
     uint32_t* sa = sa_all + (size_t)b * stride;
     uint32_t* spill = spill_all + (size_t)b * stride;
-    // pair-bucket starts, row-major over dense ids (K*K + 1 words)
-    uint32_t* pst = reinterpret_cast<uint32_t*>(grp_all + (size_t)b * bwt_group_stride(stride));
+    // the pair list (kPairCap entries at most; a block with more goes back)
+    uint64_t* pl = reinterpret_cast<uint64_t*>(grp_all + (size_t)b * bwt_group_stride(stride));
     const uint8_t* Tl = reinterpret_cast<const uint8_t*>(L.text);
+    uint32_t* W = L.w[w];
     {
         const int n16 = (n + 15) >> 4;
         const uint4* T4 = reinterpret_cast<const uint4*>(T);
         for (int v = t; v < n16; v += FT) L.text[v] = T4[v];
     }
-    // dense ids of the bytes in use (the symbol map of bwt_block_kernel mode 0)
-    uint32_t K;
-    {
-        const uint32_t pw = t < 8 ? present[(size_t)b * 8 + t] : 0u;
-        if (t < 8) L.tmp[t] = pw;
-        __syncthreads();
-        if (t < 256) {
-            uint32_t below = 0;
-            for (int q = 0; q < (t >> 5); ++q) below += (uint32_t)__popc(L.tmp[q]);
-            below += (uint32_t)__popc(L.tmp[t >> 5] & ((1u << (t & 31)) - 1u));
-            L.id[t] = (uint8_t)below;
-        }
-        uint32_t k = 0;
-        for (int q = 0; q < 8; ++q) k += (uint32_t)__popc(L.tmp[q]);
-        K = uniform(k);
+    // ---- the pair index: which second bytes follow each first byte (mask),
+    // then the non-empty pairs numbered row-major (rowpre: the number of the
+    // first pair of every 32-byte word of a row) and counted in LDS (the
+    // per-wave scratch is free until the sort phase)
+    uint32_t* cnt = &L.w[0][0];            // kPairCap pair counters, then starts, then cursors
+    uint32_t* rowpre = cnt + kPairCap;     // 256 x 8
+    if (t < 256) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) L.mask[t][j] = 0;
     }
-    const uint32_t KK = K * K;
+    if (t == 0) {
+        L.fail = 0;
+        L.nflag = 0;
+    }
+    if (t < FW) {
+        L.wlo[t] = 0xffffffffu;
+        L.whi[t] = 0;
+    }
 #ifdef BZ2MI_PHASES
     if (t < 16) L.stat[t] = 0;
 #endif
-    for (uint32_t e = t; e < KK; e += FT) L.u.cur[e] = 0;
-    if (t == 0) L.fail = 0;
     __syncthreads();
-    // ---- pair histogram, starts, scatter of every rotation into its pair bucket
     for (int i = t; i < n; i += FT) {
-        const uint32_t a = L.id[Tl[i]], c2 = L.id[Tl[i + 1 < n ? i + 1 : 0]];
-        atomicAdd(&L.u.cur[a * K + c2], 1u);
+        const uint32_t a = Tl[i], c2 = Tl[i + 1 < n ? i + 1 : 0];
+        atomicOr(&L.mask[a][c2 >> 5], 1u << (c2 & 31u));
     }
+    __syncthreads();
+    uint32_t P;
+    {
+        const uint32_t q0 = (uint32_t)t * 2;  // (first byte, word) = (q >> 3, q & 7)
+        const uint32_t c0 = (uint32_t)__popc(L.mask[q0 >> 3][q0 & 7u]), c1 = (uint32_t)__popc(L.mask[q0 >> 3][(q0 & 7u) + 1]);
+        const uint32_t ex = wg_excl_sum<FT>(c0 + c1, L.tmp, &P);
+        rowpre[q0] = ex;
+        rowpre[q0 + 1] = ex + c0;
+        if ((q0 & 7u) == 0) L.rowoff[q0 >> 3] = ex;
+    }
+    if (P > min((uint32_t)kPairCap, (uint32_t)bwt_group_stride(stride))) {  // uniform (a workgroup sum)
+        if (t == 0) redo[b] = 2u;
+        return;
+    }
+    for (uint32_t j = t; j < P; j += FT) cnt[j] = 0;
+    __syncthreads();
+    auto pair_of = [&](uint32_t a, uint32_t c2) {
+        const uint32_t wq = c2 >> 5;
+        return rowpre[a * 8 + wq] + (uint32_t)__popc(L.mask[a][wq] & ((1u << (c2 & 31u)) - 1u));
+    };
+    for (int i = t; i < n; i += FT) atomicAdd(&cnt[pair_of(Tl[i], Tl[i + 1 < n ? i + 1 : 0])], 1u);
     __syncthreads();
     {
-        uint32_t v[4], sum = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t e = (uint32_t)t * 4 + j;
-            v[j] = e < KK ? L.u.cur[e] : 0u;
-            sum += v[j];
-        }
-        uint32_t total;
-        uint32_t run = wg_excl_sum<FT>(sum, L.tmp, &total);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t e = (uint32_t)t * 4 + j;
-            if (e < KK) {
-                L.u.cur[e] = run;
-                pst[e] = run;
-                if (e % K == 0) L.cstart[e / K] = run;
-            }
-            run += v[j];
-        }
-        if (t == 0) {
-            pst[KK] = (uint32_t)n;
-            L.cstart[K] = (uint32_t)n;
+        // pair starts in place (each thread a contiguous run of pairs)
+        const uint32_t per = (P + FT - 1) / FT;
+        const uint32_t j0 = min(P, (uint32_t)t * per), j1 = min(P, j0 + per);
+        uint32_t sum = 0;
+        for (uint32_t j = j0; j < j1; ++j) sum += cnt[j];
+        uint32_t tot;
+        uint32_t run = wg_excl_sum<FT>(sum, L.tmp, &tot);
+        for (uint32_t j = j0; j < j1; ++j) {
+            const uint32_t v = cnt[j];
+            cnt[j] = run;
+            run += v;
         }
     }
     __syncthreads();
-    for (int i = t; i < n; i += FT) {
-        const uint32_t a = L.id[Tl[i]], c2 = L.id[Tl[i + 1 < n ? i + 1 : 0]];
-        sa[atomicAdd(&L.u.cur[a * K + c2], 1u)] = (uint32_t)i;
+    // first-byte bucket starts and the processing order (ascending size)
+    if (t <= 256) {
+        const uint32_t j = t < 256 ? rowpre[t * 8] : P;
+        L.cstart[t] = j < P ? cnt[j] : (uint32_t)n;
     }
-    // processing order: ascending first-byte bucket size (ties by byte)
-    if (t < 64) {
-        const uint32_t me = (uint32_t)t < K ? L.cstart[t + 1] - L.cstart[t] : 0xffffffffu;
+    __syncthreads();
+    if (t < 256) {
+        const uint32_t c = L.cstart[t + 1] - L.cstart[t];
         uint32_t rk = 0;
-        for (uint32_t q = 0; q < K; ++q) {
+        for (uint32_t q = 0; q < 256; ++q) {
             const uint32_t o = L.cstart[q + 1] - L.cstart[q];
-            rk += (o < me || (o == me && q < (uint32_t)t)) ? 1u : 0u;
+            rk += (o < c || (o == c && q < (uint32_t)t)) ? 1u : 0u;
         }
-        if ((uint32_t)t < K) {
-            L.order[rk] = (uint8_t)t;
-            L.rank[t] = (uint8_t)rk;
+        L.order[rk] = (uint8_t)t;
+        L.rank[t] = (uint8_t)rk;
+    }
+    // the buckets in the order before s_big are sorted whole (no copies into
+    // them); the last kCopySteps non-empty ones are the copy-processed buckets
+    const uint32_t K = (uint32_t)__syncthreads_count(t < 256 && L.cstart[t + 1] > L.cstart[t]);
+    const uint32_t s0 = 256u - K;
+    const uint32_t s_big = max(s0, 256u - (uint32_t)kCopySteps);
+    // the pair list (global): start, length, bytes, sorted-explicitly flag
+    for (uint32_t q = t; q < 2048; q += FT) {
+        const uint32_t a = q >> 3, wq = q & 7u;
+        uint32_t m = L.mask[a][wq], j = rowpre[q];
+        const uint32_t ra = L.rank[a];
+        while (m) {
+            const uint32_t c2 = wq * 32 + (uint32_t)__builtin_ctz(m);
+            m &= m - 1;
+            const uint32_t st = cnt[j], en = j + 1 < P ? cnt[j + 1] : (uint32_t)n;
+            pl[j] = pe_make(st, en - st, c2, a, L.rank[c2] >= ra || ra < s_big);
+            ++j;
         }
     }
+    __syncthreads();
+    // ---- every rotation to its pair bucket
+    for (int i = t; i < n; i += FT)
+        sa[atomicAdd(&cnt[pair_of(Tl[i], Tl[i + 1 < n ? i + 1 : 0])], 1u)] = (uint32_t)i;
     __threadfence_block();
     __syncthreads();
 #ifdef BZ2MI_PHASES
     if (t == 0) atomicAdd(&g_tbk_stat[0], wall_clock64() - tk0);
 #endif
-    uint32_t* W = L.u.w[w];
-    TBK_T(1, K);
+    TBK_T(1, P);
     // ---- sort phase: the pair buckets (a, c) with rank(c) >= rank(a) are
     // sorted directly (the others are filled by the copies below), all at
-    // once: round 0 deals the pair buckets over the waves, partitions put
-    // their children into the next round's list; a round ends at a barrier
+    // once: round 0 deals the pair buckets over the waves in equal shares of
+    // work (contiguous ranges of the pair list), partitions put their
+    // children into the next round's list; a round ends at a barrier
 #ifdef BZ2MI_PHASES
     tk1 = wall_clock64();
 #endif
     if (t < 2) L.qn[t] = 0;
-    __syncthreads();
     {
-        // deal the pair buckets to the waves in equal shares of work
-        uint32_t wk[4], sum = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t e = (uint32_t)t * 4 + j;
-            wk[j] = 0;
-            if (e < KK) {
-                const uint32_t a = e / K, c2 = e - a * K, len = pst[e + 1] - pst[e];
-                if (len >= 2 && L.rank[c2] >= L.rank[a]) wk[j] = text_work(len);
-            }
-            sum += wk[j];
+        const uint32_t per = (P + FT - 1) / FT;
+        const uint32_t e0 = (uint32_t)t * per, e1 = min(P, e0 + per);
+        uint32_t sum = 0;
+        for (uint32_t e = e0; e < e1; ++e) {
+            const uint64_t v = pl[e];
+            const uint32_t len = pe_len(v);
+            if (pe_expl(v) && len >= 2) sum += text_work(len);
         }
         uint32_t total;
         uint32_t run = wg_excl_sum<FT>(sum, L.tmp, &total);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t e = (uint32_t)t * 4 + j;
-            if (e < KK) L.own[e] = wk[j] ? text_owner(run, wk[j], total) : (uint8_t)(e % FW);
-            run += wk[j];
+        for (uint32_t e = e0; e < e1; ++e) {
+            const uint64_t v = pl[e];
+            const uint32_t len = pe_len(v);
+            if (!pe_expl(v)) continue;
+            if (len == 1) {
+                const uint32_t st = pe_start(v);
+                text_final(Tl, n, st, ld_fresh(sa + st), out, orig);
+                continue;
+            }
+            const uint32_t wk = text_work(len);
+            const uint32_t o = text_owner(run, wk, total);
+            run += wk;
+            pl[e] = v | ((uint64_t)o << 51);
+            atomicMin(&L.wlo[o], e);
+            atomicMax(&L.whi[o], e + 1);
         }
     }
+    __threadfence_block();
     __syncthreads();
-    for (uint32_t e0 = 0; e0 < KK; e0 += 64) {  // scalar loop over the pair buckets
-        const uint32_t e = e0 + (uint32_t)lane;
-        const bool mine = e < KK && L.own[e] == (uint8_t)w;
-        if (!__ballot(mine)) continue;
-        const uint32_t a = e / K, c2 = e - a * K;
-        const uint32_t st = mine ? pst[e] : 0u, len = mine ? pst[e + 1] - st : 0u;
-        const bool expl = mine && len > 0 && L.rank[c2] >= L.rank[a];
-        if (expl && len == 1) text_final(Tl, n, st, ld_fresh(sa + st), out, orig);
-        for (uint64_t m = __ballot(expl && len >= 2); m; m &= m - 1) {
-            if (uniform(*(volatile uint32_t*)&L.fail)) break;  // the block goes back to the general path
-            const int l = __builtin_ctzll(m);
-            const Seg seg{uniform((uint32_t)__shfl((int)st, l)), uniform((uint32_t)__shfl((int)len, l))};
-            TBK_T(2, seg.len);
+    {
+        const uint32_t lo = uniform(L.wlo[w]), hi = uniform(L.whi[w]);
+        for (uint32_t e0 = lo; e0 < hi; e0 += 64) {
+            const uint32_t e = e0 + (uint32_t)lane;
+            const uint64_t v = e < hi ? pl[e] : 0ull;
+            const bool mine = e < hi && pe_expl(v) && pe_len(v) >= 2 && pe_owner(v) == (uint32_t)w;
+            for (uint64_t m = __ballot(mine); m; m &= m - 1) {
+                if (uniform(*(volatile uint32_t*)&L.fail)) break;  // the block goes back to the general path
+                const int l = __builtin_ctzll(m);
+                const uint32_t vs = (uint32_t)__shfl((int)(uint32_t)v, l);
+                const uint32_t vl = (uint32_t)__shfl((int)(uint32_t)(v >> 17), l);
+                const Seg seg{uniform(vs & 0x1ffffu), uniform(vl & 0x1ffffu)};
+                TBK_T(2, seg.len);
 #ifdef BZ2MI_PHASES
-            const unsigned long long ti0 = wall_clock64();
+                const unsigned long long ti0 = wall_clock64();
 #endif
-            if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, 2, out, orig, W, L);
-            else text_partition(Tl, n, sa, spill, seg, 2, out, orig, W, L, 0);
-            TBK_T(10, seg.len);
+                if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, 2, out, orig, W, L);
+                else text_partition(Tl, n, sa, spill, seg, 2, out, orig, W, L, 0);
+                TBK_T(10, seg.len);
 #ifdef BZ2MI_PHASES
-            TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
+                TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
 #endif
+            }
         }
     }
     __threadfence_block();
@@ -2856,39 +3269,91 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
     tks = wall_clock64() - tk1;
 #endif
-    // ---- copy steps in ascending bucket size: bucket ss is complete (its
-    // sorted pair buckets, and (ss, c) for every earlier c from that step's
-    // copy); it fills (x, ss) for every later x
+    // ---- copy steps.  The pair starts go to LDS (the per-wave scratch is
+    // free now: 16 x 256 copy counters, then the starts).
     const uint32_t failed = uniform(L.fail);
-    for (uint32_t s = 0; s < K && !failed; ++s) {
+    uint32_t* pstart = &L.w[0][0] + FW * 256;
+    for (uint32_t j = t; j <= P; j += FT) pstart[j] = j < P ? pe_start(pl[j]) : (uint32_t)n;
+    __syncthreads();
+    // (a) the buckets before s_big were sorted whole (every pair explicit):
+    // their copies are independent -- a wave per source bucket fills (x, ss)
+    // for every copy-processed x at once
+    if (!failed && s_big > s0) {
+        uint32_t* C = &L.w[0][0] + w * 256;  // this wave's cursor per x (0xffffffff: not a target)
+        for (uint32_t s = s0 + (uint32_t)w; s < s_big; s += FW) {
+            const uint32_t ss = L.order[s];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t x = (uint32_t)lane * 4 + j, wq = ss >> 5, bit = ss & 31u;
+                const uint32_t mw = L.mask[x][wq];
+                uint32_t c = 0xffffffffu;
+                if (L.rank[x] >= s_big && ((mw >> bit) & 1u)) {
+                    uint32_t q = L.rowoff[x] + (uint32_t)__popc(mw & ((1u << bit) - 1u));
+                    for (uint32_t r = 0; r < wq; ++r) q += (uint32_t)__popc(L.mask[x][r]);
+                    c = pstart[q];
+                }
+                C[x] = c;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t cs = L.cstart[ss], ce = L.cstart[ss + 1];
+            for (uint32_t k0 = cs; k0 < ce; k0 += 64) {
+                const uint32_t k = k0 + (uint32_t)lane;
+                const uint32_t v = k < ce ? ld_fresh(sa + k) : 0u;
+                const uint32_t i = v & 0x1ffffu;
+                const uint32_t j = i ? i - 1 : (uint32_t)n - 1;
+                const uint32_t x = k < ce ? (uint32_t)Tl[j] : 0u;
+                const uint32_t bs = C[x];
+                const bool tgt = k < ce && bs != 0xffffffffu;
+                const uint64_t peers = wave_match8(x, tgt);
+                if (tgt) {
+                    const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
+                    sa[bs + below] = j | (v & kUnres);
+                    text_final(Tl, n, bs + below, j, out, orig);
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (tgt && (peers & __lanemask_lt()) == 0) C[x] = bs + (uint32_t)__popcll(peers);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    // (b) the copy-processed buckets in ascending size: bucket ss is complete
+    // (its sorted pair buckets, and (ss, c) for every earlier c from that
+    // step's copy); it fills (x, ss) for every later x
+    for (uint32_t s = s_big; s < 256 && !failed; ++s) {
         const uint32_t ss = L.order[s];
         TBK_T(5, s);
 #ifdef BZ2MI_PHASES
         tk1 = wall_clock64();
 #endif
-        if (w == 0) {
-            const bool in = (uint32_t)lane < K;
-            const bool tg = in && L.rank[lane] > s && pst[lane * K + ss + 1] > pst[lane * K + ss];
-            if (in) {
-                L.target[lane] = tg ? 1 : 0;
-                L.pcol[lane] = pst[lane * K + ss];
+        bool tg = false;
+        if (t < 256) {
+            const uint32_t x = (uint32_t)t, wq = ss >> 5, bit = ss & 31u;
+            const uint32_t mw = L.mask[x][wq];
+            tg = L.rank[x] > s && ((mw >> bit) & 1u);
+            if (tg) {
+                uint32_t j = L.rowoff[x] + (uint32_t)__popc(mw & ((1u << bit) - 1u));
+                for (uint32_t q = 0; q < wq; ++q) j += (uint32_t)__popc(L.mask[x][q]);
+                L.pcol[x] = pstart[j];
             }
+            L.target[x] = tg ? 1 : 0;
         }
-        __syncthreads();
-        // ---- copy phase: bucket ss is in order; (x, ss) = the rotations i-1 of
-        // it with T[i-1] = x, in that order, for every later x.  Chunks of
-        // FW * kCopyR * 64 rotations: every wave loads its kCopyR * 64 at once,
+        // bucket ss is in order; (x, ss) = the rotations i-1 of it with
+        // T[i-1] = x, in that order, for every later x.  Chunks of FW *
+        // kCopyR * 64 rotations: every wave loads its kCopyR * 64 at once,
         // counts its targets per x, a scan over the waves gives each wave its
         // first slot per x (carried from chunk to chunk in pcol), then the
-        // stable placement from registers
-        bool any = false;
-        for (uint32_t x = 0; x < K; ++x) any |= L.target[x] != 0;
-        if (uniform(any ? 1u : 0u)) {
+        // stable placement from registers.  A flagged source gives a flagged
+        // target.
+        if (__syncthreads_or(tg ? 1 : 0)) {
+            uint32_t* C = &L.w[0][0] + w * 256;
             const uint32_t cs = L.cstart[ss], ce = L.cstart[ss + 1];
             for (uint32_t c0 = cs; c0 < ce; c0 += FW * kCopyR * 64) {
                 const uint32_t w0 = c0 + (uint32_t)w * (kCopyR * 64);
                 uint32_t jv[kCopyR], xv[kCopyR];
-                W[lane] = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) C[lane * 4 + j] = 0;
 #pragma unroll
                 for (int r = 0; r < kCopyR; ++r) {
                     const uint32_t k = w0 + (uint32_t)(r * 64 + lane);
@@ -2898,19 +3363,21 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #pragma unroll
                 for (int r = 0; r < kCopyR; ++r) {
                     const bool v = jv[r] != 0xffffffffu;
-                    const uint32_t j = jv[r] ? jv[r] - 1 : (uint32_t)n - 1;
-                    const uint32_t x = v ? L.id[Tl[j]] : 0u;
-                    const bool tg = v && L.target[x];
-                    jv[r] = j;
-                    xv[r] = tg ? x : 0xffu;
-                    if (tg) atomicAdd(&W[x], 1u);
+                    const uint32_t i = jv[r] & 0x1ffffu;
+                    const uint32_t j = i ? i - 1 : (uint32_t)n - 1;
+                    const uint32_t x = v ? (uint32_t)Tl[j] : 0u;
+                    const bool tgt = v && L.target[x];
+                    jv[r] = j | (jv[r] & kUnres);
+                    xv[r] = tgt ? x : 0x100u;
+                    if (tgt) atomicAdd(&C[x], 1u);
                 }
                 __syncthreads();
-                if ((uint32_t)t < K) {
+                if (t < 256) {
                     uint32_t run = L.pcol[t];
+                    uint32_t* c0p = &L.w[0][0] + t;
                     for (int q = 0; q < FW; ++q) {
-                        const uint32_t v = L.u.w[q][t];
-                        L.u.w[q][t] = run;
+                        const uint32_t v = c0p[q * 256];
+                        c0p[q * 256] = run;
                         run += v;
                     }
                     L.pcol[t] = run;
@@ -2919,15 +3386,15 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #pragma unroll
                 for (int r = 0; r < kCopyR; ++r) {
                     const uint32_t x = xv[r];
-                    const bool tg = x != 0xffu;
-                    const uint64_t peers = wave_match6(x, tg);
-                    const uint32_t bs = tg ? W[x] : 0u;
-                    if (tg) {
+                    const bool tgt = x != 0x100u;
+                    const uint64_t peers = wave_match8(x, tgt);
+                    const uint32_t bs = tgt ? C[x & 255u] : 0u;
+                    if (tgt) {
                         const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
                         const uint32_t pos = bs + below;
                         sa[pos] = jv[r];
-                        text_final(Tl, n, pos, jv[r], out, orig);
-                        if (below == 0) W[x] = bs + (uint32_t)__popcll(peers);
+                        text_final(Tl, n, pos, jv[r] & 0x1ffffu, out, orig);
+                        if (below == 0) C[x] = bs + (uint32_t)__popcll(peers);
                     }
                     __builtin_amdgcn_wave_barrier();
                 }
@@ -2939,6 +3406,19 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         tkc += wall_clock64() - tk1;
 #endif
     }
+    // ---- deferred runs (long repeats): prefix doubling over the flagged runs
+#ifdef BZ2MI_PHASES
+    const unsigned long long tkr0 = wall_clock64();
+#endif
+    if (!failed && uniform(L.nflag)) {
+        uint32_t* key = reinterpret_cast<uint32_t*>(key_all + (size_t)b * tcap);
+        uint32_t* glist = reinterpret_cast<uint32_t*>(glist_all + (size_t)b * tcap);
+        text_resolve(Tl, n, sa, spill, key, glist, out, orig, L);
+    }
+#ifdef BZ2MI_PHASES
+    const unsigned long long tkr = wall_clock64() - tkr0;
+#endif
+    __syncthreads();
     if (t == 0 && L.fail) redo[b] = 2u;
     TBK_T(6, L.fail);
 #ifdef BZ2MI_PHASES
@@ -2947,7 +3427,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         atomicAdd(&g_tbk_stat[2], tkc);
         atomicAdd(&g_tbk_stat[8], 1ull);
         atomicAdd(&g_tbk_stat[9], wall_clock64() - tk0);
-        atomicAdd(&g_tbk_stat[11], (unsigned long long)K);
+        atomicAdd(&g_tbk_stat[11], (unsigned long long)L.nflag);
+        atomicAdd(&g_tbk_stat[14], tkr);
+        atomicMax(&g_tbk_stat[15], wall_clock64() - tk0);
         for (int k = 3; k < 8; ++k) atomicAdd(&g_tbk_stat[k], (unsigned long long)L.stat[k]);
         for (int k = 10; k < 14; ++k)
             if (k != 11) atomicAdd(&g_tbk_stat[k], (unsigned long long)L.stat[k]);

@@ -31,20 +31,24 @@ __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const ui
 // small buckets in one launch, the block's text held in LDS (1024 threads, one
 // workgroup per CU).  Large buckets still go to the level queue.
 constexpr int kBwtLdsText = 90112;
-// mode 0: every block, except that text-like ones (few distinct bytes) only
-// get their symbol map and redo[b] = 1 (redo zeroed before): they go to
-// bwt_text_kernel; mode 1: the blocks bwt_text_kernel handed back (redo[b] = 2)
+// mode 0: every block, except that text-like ones (most rotations in large
+// first-byte buckets) only get their symbol map and redo[b] = 1 (redo zeroed
+// before): they go to bwt_text_kernel; mode 1: the blocks bwt_text_kernel
+// handed back (redo[b] = 2)
 __global__ void bwt_block_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                                  uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, BwtItem* lq,
                                  uint32_t* lcount, size_t lcap, uint32_t* present_out, uint64_t* tl,
                                  uint32_t* tcount, size_t tcap, uint32_t* redo, int mode, uint64_t* squeue,
                                  uint32_t* scount, size_t scap);
-// text-like blocks (redo[b] == 1): induced sorting with the text in LDS;
-// SA and BWT bytes complete, or redo[b] = 2.  `spill_all` (stride words per
-// block) and `grp_all` (the pair-bucket table) are scratch.
+// text-like blocks (redo[b] == 1): induced sorting with the text in LDS, deep
+// ties ordered by prefix doubling; SA and BWT bytes complete, or redo[b] = 2.
+// Scratch: `spill_all` (stride words per block), `grp_all` (the pair list),
+// `key_all` / `glist_all` (tcap uint64 per block: the doubling keys and group
+// lists; the tie queues of bwt_block_kernel, unused by text blocks).
 __global__ void bwt_text_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
-                                uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, const uint32_t* present,
-                                uint32_t* redo, uint32_t* spill_all, BwtSeg* grp_all);
+                                uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint32_t* redo,
+                                uint32_t* spill_all, BwtSeg* grp_all, uint64_t* key_all, uint64_t* glist_all,
+                                size_t tcap);
 __global__ void redo_all_kernel(uint32_t* redo, int nblocks);
 __global__ void bwt_level_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                  uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,

@@ -97,6 +97,8 @@ def cases():
     yield "rnd64k", synth.random_bytes(65536).tobytes()
     yield "runs64k", synth.runs_bytes(65536).tobytes()
     yield "acgt64k", synth.small_alphabet_bytes(65536).tobytes()
+    # round 4: enwik9-like text (~150 distinct bytes, markup, UTF-8) -- C3
+    yield "rtext64k", synth.realtext_bytes(65536).tobytes()
     # a block whose RLE1 length reaches exactly S at -1 (H1)
     yield "h1_exact", find_h1()
 

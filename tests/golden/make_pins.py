@@ -13,7 +13,10 @@ BitOutputStream / CRC32 compiled from /root/reference) at
     run-heavy bytes (32 blocks: every slot of p = 10 is reused three times);
   * -1 (S = 10,000), p = 10 on the same inputs (~290 blocks);
   * O_ref900 (the 900 KB mode, Config.hpp:30 BLOCKSIZE_DEFAULT = 100000):
-    -9 at p = 10 and 3 on 12 MiB of random, text and mixed bytes (14 blocks).
+    -9 at p = 10 and 3 on 12 MiB of random, text and mixed bytes (14 blocks);
+  * round 4: the enwik9-like C3 text (synth.realtext_bytes: ~150 distinct
+    bytes per 90 KB block) and its long-repeat variant (synth.repeats_bytes)
+    at -9 p = 10/3/1 and -1, and the realtext in the 900 KB mode.
 
 Only the SHA-256 and length of each output are stored (tests/golden/pins.json),
 with the SHA-256 of the input so generator drift is caught.  Run in the build
@@ -44,11 +47,18 @@ INPUTS = {
     "rnd12m": ("random", 12 << 20),
     "txt12m": ("text", 12 << 20),
     "mix12m": ("mixed", 12 << 20),
+    "rtx2m75": ("realtext", 2_883_584),
+    "rep2m75": ("repeats", 2_883_584),
+    "rtx12m": ("realtext", 12 << 20),
 }
 
 PINS = [(name, level, p, 10000) for name in ("rnd2m75", "txt2m75", "mix2m75", "run2m75")
         for level, p in ((9, 10), (9, 3), (9, 1), (1, 10))]
 PINS += [(name, 9, p, 100000) for name in ("rnd12m", "txt12m", "mix12m") for p in (10, 3)]
+# round 4: C3 enwik9-like text (synth.realtext_bytes, ~150 distinct bytes per
+# block) and its long-repeat stress variant (synth.repeats_bytes)
+PINS += [(name, level, p, 10000) for name in ("rtx2m75", "rep2m75") for level, p in ((9, 10), (9, 3), (9, 1), (1, 10))]
+PINS += [("rtx12m", 9, p, 100000) for p in (10, 3)]
 
 
 def make_input(name: str) -> bytes:
@@ -58,6 +68,10 @@ def make_input(name: str) -> bytes:
         return synth.random_bytes(n, seed).tobytes()
     if kind == "text":
         return synth.text_bytes(n, seed).tobytes()
+    if kind == "realtext":
+        return synth.realtext_bytes(n, seed).tobytes()
+    if kind == "repeats":
+        return synth.repeats_bytes(n, seed).tobytes()
     if kind == "runs":  # runs of 1..12: RLE1 pieces of every length, ~19 blocks at -9
         return synth.runs_bytes(n, seed, max_run=12).tobytes()
     return synth.mixed_bytes(n, seed, segment=512 << 10).tobytes()

@@ -46,9 +46,16 @@ def test_golden_streams(bz, manifest):
             assert bz.compress(data, st["level"], st["p"]) == golden_file(st["file"]), (name, st)
 
 
+def _repeats(n: int) -> np.ndarray:
+    from bz2mi import synth
+    return synth.repeats_bytes(n)
+
+
 def _inputs():
     from bz2mi import synth
     yield "text", synth.text_bytes(6 << 20)
+    yield "realtext", synth.realtext_bytes(6 << 20)
+    yield "realtext_repeats", _repeats(4 << 20)
     yield "random", synth.random_bytes(6 << 20)
     yield "runs", synth.runs_bytes(6 << 20)
     yield "acgt", synth.small_alphabet_bytes(3 << 20)
@@ -70,7 +77,8 @@ def test_seeded_inputs_match_cpuref(bz, cpuref, level, p):
 
 def test_900k_mode_matches_cpuref(bz, cpuref):
     from bz2mi import synth
-    for data in (synth.text_bytes(5 << 20).tobytes(), synth.random_bytes(3 << 20).tobytes()):
+    for data in (synth.text_bytes(5 << 20).tobytes(), synth.random_bytes(3 << 20).tobytes(),
+                 synth.realtext_bytes(6 << 20).tobytes(), _repeats(4 << 20).tobytes()):
         want = cpuref.compress(data, 9, 10, unit=100000, threads=16)
         got = bz.compress(data, 9, 10, unit=100000)
         assert got == want

@@ -8,7 +8,15 @@ import bz2mi
 from bz2mi import synth
 
 n = int(os.environ.get("MIB", "256")) << 20
-x = torch.from_numpy(synth.text_bytes(n, synth.SEED_TEXT)).cuda()
+kind = os.environ.get("DATA", "text")
+if kind == "realtext":
+    x = torch.from_numpy(synth.realtext_bytes(n, threads=8)).cuda()
+elif kind == "repeats":
+    sys.path.insert(0, os.path.join(R, "tests"))
+    from test_gpu import _repeats
+    x = torch.from_numpy(_repeats(n)).cuda()
+else:
+    x = torch.from_numpy(synth.text_bytes(n, synth.SEED_TEXT)).cuda()
 ctx = bz2mi.Context(9, 10)
 out = torch.empty(n + n // 8 + (1 << 20), dtype=torch.uint8, device="cuda")
 ctx.compress_device(x.data_ptr(), n, out.data_ptr(), out.numel())
@@ -19,7 +27,8 @@ print("rc", L.bz2mi_debug_phases(4, buf))
 v = list(buf)
 nb = max(1, v[8])
 print(f"blocks {v[8]}  per block: total {v[9] / nb / 100:.1f} us, setup {v[0] / nb / 100:.1f}, sort {v[1] / nb / 100:.1f}, "
-      f"copy {v[2] / nb / 100:.1f};  steps {v[11] / nb:.1f}, rounds {v[3] / nb:.1f}")
+      f"copy {v[2] / nb / 100:.1f}, resolve {v[14] / nb / 100:.1f}, slowest block {v[15] / 100:.1f};  "
+      f"flagged {v[11] / nb:.1f}, rounds {v[3] / nb:.1f}")
 print(f"  sorts {v[4] / nb:.1f} ({v[7] / nb:.0f} elems, tie rounds {v[10] / nb:.1f}), partitions {v[5] / nb:.1f} "
       f"({v[6] / nb:.0f} elems)")
 print(f"  wave-busy per block: sorts {v[12] / nb / 100:.1f} us, partitions {v[13] / nb / 100:.1f} us "
