@@ -85,8 +85,10 @@ def stage_traffic(args, stage):
 
 
 def host_cpu() -> dict:
-    """Host CPU model and the cores this process may use (the GPU box gives a
-    1-GPU job a share of the machine: os.sched_getaffinity, at most 16)."""
+    """Host CPU model and the cores this process may use: the GPU box gives a
+    1-GPU job a share of the machine (OMP_NUM_THREADS / MAX_JOBS = 16 there,
+    while os.sched_getaffinity lists every core of the host), so the parallel
+    baseline uses that share, capped by the affinity mask."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -100,7 +102,15 @@ def host_cpu() -> dict:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    return {"model": model, "cores_available": avail, "cores_used_parallel": max(1, min(16, avail))}
+    share = 0
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        try:
+            share = max(share, int(os.environ.get(var, "0")))
+        except ValueError:
+            pass
+    used = max(1, min(avail, share if share > 0 else avail))
+    return {"model": model, "cores_in_affinity_mask": avail, "job_cpu_share": share or None,
+            "cores_used_parallel": used}
 
 
 def cpu_baseline(sample_bytes: int) -> dict:
@@ -151,7 +161,8 @@ def cpu_baseline(sample_bytes: int) -> dict:
         dt = time.perf_counter() - t0
         if res is not None and n >= 0:
             res["all_cores"] = {"value": round(len(data) / dt / 1e6, 3), "unit": "MB/s", "threads": th,
-                                "what": "cpu_ref block-parallel on a pthread pool, same bytes as O_ref"}
+                                "what": "cpu_ref block-parallel on a pthread pool, same bytes as O_ref, on every "
+                                        "core this job may use (host_cpu: the job's CPU share)"}
     if res is None:
         return None
     sub = data[: min(len(data), 32 << 20)]
@@ -208,6 +219,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-900k", action="store_true", help="skip the 900 KB-mode measurement beside the line")
+    ap.add_argument("--no-units", action="store_true",
+                    help="N = 1: skip the unit-protocol line (4 units, the code N > 1 times) beside the line")
     ap.add_argument("--mode", choices=["compress", "decompress", "e2e"], default="compress",
                     help="compress = the bench line (BASELINE metric); decompress = configs[4]: device "
                          "decompression of the stream this run compresses (output MB/s); e2e = file -> file "
@@ -219,10 +232,10 @@ def main():
     ap.add_argument("--units-per-gpu", type=int, default=None,
                     help="units of the logical stream per rank (interleaved over the ranks); N > 1 default 4; "
                          "given at N = 1, the unit protocol runs on the one device (the base of a 1 -> N curve)")
-    ap.add_argument("--gather", choices=["none", "rank0"], default="none",
-                    help="N > 1: rank0 = also gather the stream onto rank 0 over RCCL inside the timed step; "
-                         "none = the stream ends distributed (each rank holds its units' final bytes), the "
-                         "gather is then timed once after the steps and reported beside the line")
+    ap.add_argument("--gather", choices=["none", "rank0"], default="rank0",
+                    help="N > 1: rank0 (default) = the ordered RCCL gather of the stream onto rank 0 is inside "
+                         "the timed step, so the value is a whole .bz2 on one rank; none = the stream ends "
+                         "distributed (each rank holds its units' final bytes), the gather timed once after")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -369,6 +382,24 @@ def main():
                    "what": "the same input and steps at -9 in the 900 KB mode (unit 100000; O_ref900 pins)"}
         del out9
         ctx9.close()
+    # the code the N > 1 lines time, at N = 1: the same workload as 4 units of
+    # one logical stream through bz2mi.shard (the base of the 1 -> N curve)
+    units_n1 = None
+    if not args.no_units and world == 1 and args.mode == "compress":
+        import copy
+        del out
+        ctx.close()
+        torch.cuda.empty_cache()
+        a2 = copy.copy(args)
+        a2.units_per_gpu, a2.no_cpu = 4, True
+        u = bench_units(a2, 1, emit=False)
+        units_n1 = {k: u[k] for k in ("value", "ms_per_step")}
+        units_n1.update({"units": 4, "decode_check": u["config"]["decode_check"],
+                         "gather_in_step": u["config"]["gather_in_step"],
+                         "stage_ms": u["roofline"]["stage_ms_rank0"],
+                         "what": "the same data shape as 4 units of 256 MiB through the unit protocol (chain token, "
+                                 "seed-sum token, bit offsets, assembly, ordered gather) on this one device: the "
+                                 "code the N > 1 lines time"})
     cpu = None if args.no_cpu else cpu_baseline(args.cpu_sample_mib << 20)
     refgpu = None if args.no_cpu else reference_gpu(64 << 20)
     line = {
@@ -381,6 +412,7 @@ def main():
                    "blocks": nb, "parallelism": "dp1 (one stream, one device call)", "decode_check": verified},
         "roofline": roof,
         "mode_900k": mode900,
+        "unit_protocol_n1": units_n1,
         "cpu_baseline": cpu,
         "reference_on_this_gpu": refgpu,
     }
@@ -406,7 +438,7 @@ def unit_bytes(args, g: int, U: int, dev):
     return torch.from_numpy(synth.mixed_bytes(U, synth.SEED_MIXED, seg, first_segment=g * (U // seg))).to(dev)
 
 
-def bench_units(args, world: int):
+def bench_units(args, world: int, emit: bool = True):
     """N ranks, one logical stream (SURVEY.md section 8(e), config C4's layout):
     world x units-per-gpu units of U = mib/units-per-gpu MiB, unit g on rank
     g mod world; every unit buffer = its bytes + the tail halo (the bytes of the
@@ -577,10 +609,15 @@ def bench_units(args, world: int):
                 "value_with_gather": round(tot_in / ((ms_step + (0 if gather_in else gather_ms)) * 1e-3) / 1e6, 2)},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        if emit:
+            print(json.dumps(line), flush=True)
     barrier()
     if world > 1:
         dist.destroy_process_group()
+    for g in mine:
+        units[g].close()
+    ctx.close()
+    return line if rank == 0 else None
 
 
 WORKLOAD_DATA = {"random": "random bytes, unit g seeded 0x5EED0001+g", "text": "word-Markov text, unit g seeded "

@@ -20,6 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BZ2MI_LIBRARY") or os.path.join(_HERE, "libbz2mi.so")
 
 BZ2MI_OK = 0
+ABI_VERSION = 4  # include/bz2mi.h BZ2MI_ABI_VERSION
 BZ2MI_EINVAL = -1
 BZ2MI_EDEVICE = -2
 BZ2MI_ESPACE = -3
@@ -35,7 +36,7 @@ EXPORTS = (
     "bz2mi_dlast_timings", "bz2mi_unit_halo", "bz2mi_unit_create", "bz2mi_unit_destroy", "bz2mi_unit_begin",
     "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode", "bz2mi_unit_assemble", "bz2mi_unit_timings",
     "bz2mi_unit_stats", "bz2mi_host_alloc", "bz2mi_host_free", "bz2mi_unit_begin_host", "bz2mi_unit_assemble_host",
-    "bz2mi_dstream_reset", "bz2mi_dstream",
+    "bz2mi_dstream_reset", "bz2mi_dstream", "bz2mi_dlast_trailing", "bz2mi_abi_version",
 )
 
 _lib = None
@@ -99,6 +100,11 @@ def lib() -> ctypes.CDLL:
                                     c.c_size_t, c.POINTER(c.c_uint64), c.POINTER(c.c_size_t), c.POINTER(c.c_int)]
     L.bz2mi_dlast_timings.restype = c.c_int
     L.bz2mi_dlast_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
+    L.bz2mi_dlast_trailing.restype = c.c_int
+    L.bz2mi_dlast_trailing.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
+    L.bz2mi_abi_version.restype = c.c_int
+    if L.bz2mi_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI {L.bz2mi_abi_version()}, this binding expects {ABI_VERSION}")
     L.bz2mi_unit_halo.restype = c.c_size_t
     L.bz2mi_unit_halo.argtypes = [c.c_int, c.c_int]
     L.bz2mi_unit_create.restype = c.c_void_p
@@ -328,6 +334,8 @@ class Decompressor:
     `concatenated`: decode every stream of the input (bzip2's behaviour); by
     default only the first, as the reference's InputStream does."""
 
+    last_trailing = 0  # input bytes after the last decoded stream (ignored) of the last decompress()
+
     def __init__(self, unit: int = 10000, device: int = 0, concatenated: bool = False):
         L = lib()
         h = L.bz2mi_dcreate(unit, device)
@@ -378,6 +386,14 @@ class Decompressor:
                 continue
             if rc != BZ2MI_OK:
                 self._raise(rc)
+            tr = ctypes.c_uint64(0)
+            _check(lib().bz2mi_dlast_trailing(self._h, ctypes.byref(tr)))
+            self.last_trailing = tr.value
+            if tr.value and bytes(src[src.size - tr.value:src.size - tr.value + 3]) == b"BZh":
+                import warnings
+                warnings.warn(f"{tr.value} bytes after the end of the first stream start another .bz2 stream and "
+                              "were not decoded (the reference's InputStream reads one stream; "
+                              "Decompressor(concatenated=True) decodes them all)", stacklevel=2)
             return out[: n.value].tobytes()
         raise RuntimeError("decompress: output size changed between attempts")
 

@@ -291,6 +291,10 @@ class DeviceUnit:
     def stats(self):
         return self.unit.stats()
 
+    def close(self) -> None:
+        self.unit.close()
+        self._out = None
+
 
 def settle(lay: Layout, ctl_group=None) -> dict:
     """Make this rank's device pieces disjoint: where a unit starts mid-byte,

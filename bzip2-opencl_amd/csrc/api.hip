@@ -146,10 +146,13 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     uint32_t* tc[2] = {c->d_tc, c->d_tc + c->bwtq_blocks};
     uint32_t* p2count = t.d_bcnt + 768;
     uint32_t* pull = t.d_bcnt + 769;
-    static const bool lds_text = [] {
-        const char* e = getenv("BZ2MI_LDSTEXT");
-        return !(e && *e == '0');
-    }();
+    // A/B builds only (-DBZ2MI_AB_NO_LDSTEXT / _NO_TEXTBWT / _NO_WLEVEL): the
+    // product has no run-time path switches
+#ifdef BZ2MI_AB_NO_LDSTEXT
+    constexpr bool lds_text = false;
+#else
+    constexpr bool lds_text = true;
+#endif
     // LDS-text path (blocks fit in LDS): the small batches of the levels go to
     // per-block lists (counts d_scb, capacity tcap each) instead of the shards
     const bool blk = lds_text && c->S <= kBwtLdsText;
@@ -161,10 +164,11 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         HIPCHECK(hipMemsetAsync(t.d_redo, 0, nb * sizeof(uint32_t), s));
         // mode 0 defers text-like blocks to the induced-sorting text kernel,
         // mode 1 takes the ones it hands back
-        static const bool text_path = [] {
-            const char* e = getenv("BZ2MI_TEXTBWT");
-            return !(e && *e == '0');
-        }();
+#ifdef BZ2MI_AB_NO_TEXTBWT
+        constexpr bool text_path = false;
+#else
+        constexpr bool text_path = true;
+#endif
         for (int mode = 0; mode < 2; ++mode) {
             if (mode == 1 && text_path) {
                 hipLaunchKernelGGL(bwt_text_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
@@ -195,10 +199,11 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         fprintf(stderr, "[bz2mi] bwt blocks: general %u, text %u, handed back %u\n", cnt[0], cnt[1], cnt[2] + cnt[3]);
 
     }
-    static const bool wlevel = [] {
-        const char* e = getenv("BZ2MI_WLEVEL");
-        return !(e && *e == '0');
-    }();
+#ifdef BZ2MI_AB_NO_WLEVEL
+    constexpr bool wlevel = false;
+#else
+    constexpr bool wlevel = true;
+#endif
     for (int d = 1; d <= kBwtLevels; ++d) {
         if (wlevel && d < kBwtLevels) {
             hipLaunchKernelGGL(bwt_wlevel_kernel, dim3(c->wlevel_grid), dim3(256), 0, s, t.d_blocks, c->stride,
@@ -599,7 +604,8 @@ extern "C" {
 
 const char* bz2mi_last_error(void) { return g_err.c_str(); }
 
-const char* bz2mi_version(void) { return "bz2mi 0.1 (gfx950)"; }
+const char* bz2mi_version(void) { return "bz2mi 0.4 (gfx950)"; }
+int bz2mi_abi_version(void) { return BZ2MI_ABI_VERSION; }
 
 int bz2mi_device_count(void) {
     int n = 0;
@@ -721,7 +727,12 @@ void bz2mi_destroy(bz2mi_ctx* c) {
     for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB, c->sF})
         if (st) (void)hipStreamSynchronize(st);
     std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_sq, c->d_lq[0], c->d_lq[1], c->d_tq[0], c->d_tq[1],
-                               c->d_tc, c->d_lscratch, c->d_lspill, c->d_scb, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in};
+                               c->d_tc, c->d_lscratch, c->d_lspill, c->d_scb, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
+                               c->d_hout};
+    for (int k = 0; k < 2; ++k) {
+        if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
+        if (c->ev_pin[k]) (void)hipEventDestroy(c->ev_pin[k]);
+    }
     for (Batch& t : c->sets) free_batch(t);
     free_front(c->fe);
     for (void* p : ptrs)
@@ -816,27 +827,76 @@ int bz2mi_finish(bz2mi_ctx* c, uint8_t* out, size_t cap, size_t* out_len) {
     return BZ2MI_OK;
 }
 
+// Host bytes in and out (the reference's Memory<T> write / read around
+// kernel_close, OutputStream.hpp:83-116): the device buffers are the
+// context's and persist across calls (grown when needed), and the copies run
+// through two pinned staging buffers of kPinBytes -- the host memcpy of one
+// piece overlaps the DMA of the other.
+namespace {
+constexpr size_t kPinBytes = (size_t)16 << 20;
+
+int ensure_pinned(bz2mi_ctx* c) {
+    if (c->h_pin[0]) return BZ2MI_OK;
+    for (int k = 0; k < 2; ++k) {
+        if (hipHostMalloc((void**)&c->h_pin[k], kPinBytes, hipHostMallocDefault) != hipSuccess)
+            return fail(BZ2MI_EDEVICE, "hipHostMalloc failed");
+        HIPCHECK(hipEventCreateWithFlags(&c->ev_pin[k], hipEventDisableTiming));
+    }
+    return BZ2MI_OK;
+}
+
+int copy_in_pinned(bz2mi_ctx* c, uint8_t* d_dst, const uint8_t* in, size_t n) {
+    for (size_t off = 0, k = 0; off < n; off += kPinBytes, ++k) {
+        const size_t len = std::min(kPinBytes, n - off);
+        HIPCHECK(hipEventSynchronize(c->ev_pin[k & 1]));  // the DMA that last read this buffer is done
+        memcpy(c->h_pin[k & 1], in + off, len);
+        HIPCHECK(hipMemcpyAsync(d_dst + off, c->h_pin[k & 1], len, hipMemcpyHostToDevice, c->stream));
+        HIPCHECK(hipEventRecord(c->ev_pin[k & 1], c->stream));
+    }
+    return BZ2MI_OK;
+}
+
+int copy_out_pinned(bz2mi_ctx* c, uint8_t* out, const uint8_t* d_src, size_t n) {
+    const size_t np = (n + kPinBytes - 1) / kPinBytes;
+    for (size_t k = 0; k <= np; ++k) {
+        if (k < np) {  // piece k to pinned buffer k & 1 (its previous piece was copied out below)
+            const size_t off = k * kPinBytes, len = std::min(kPinBytes, n - off);
+            HIPCHECK(hipMemcpyAsync(c->h_pin[k & 1], d_src + off, len, hipMemcpyDeviceToHost, c->stream));
+            HIPCHECK(hipEventRecord(c->ev_pin[k & 1], c->stream));
+        }
+        if (k >= 1) {  // piece k - 1 to the caller while piece k is in flight
+            const size_t q = k - 1, off = q * kPinBytes, len = std::min(kPinBytes, n - off);
+            HIPCHECK(hipEventSynchronize(c->ev_pin[q & 1]));
+            memcpy(out + off, c->h_pin[q & 1], len);
+        }
+    }
+    return BZ2MI_OK;
+}
+}  // namespace
+
 int bz2mi_compress(bz2mi_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
     if (!c || !out_len || (n && !in)) return fail(BZ2MI_EINVAL, "null argument");
     HIPCHECK(hipSetDevice(c->device));
+    int r;
     if (n + 64 > c->in_cap) {
-        int r = dalloc(&c->d_in, n + 64);
-        if (r) return r;
+        c->in_cap = 0;
+        if ((r = dalloc(&c->d_in, n + 64))) return r;
         c->in_cap = n + 64;
     }
     const size_t dcap = bz2mi_compress_bound(n, c->level, c->unit);
-    uint8_t* d_o = nullptr;
-    HIPCHECK(hipMalloc((void**)&d_o, dcap));
-    int r = BZ2MI_OK;
-    if (n) r = hipMemcpyAsync(c->d_in, in, n, hipMemcpyHostToDevice, c->stream) == hipSuccess
-                   ? BZ2MI_OK : fail(BZ2MI_EDEVICE, "H2D copy failed");
+    if (dcap > c->hout_cap) {
+        c->hout_cap = 0;
+        if ((r = dalloc(&c->d_hout, dcap))) return r;
+        c->hout_cap = dcap;
+    }
+    if ((r = ensure_pinned(c))) return r;
+    if ((r = copy_in_pinned(c, c->d_in, in, n))) return r;
     size_t got = 0;
-    if (!r) r = compress_device_impl(c, c->d_in, n, d_o, dcap, &got);
-    if (!r && got > cap) r = fail(BZ2MI_ESPACE, "output buffer too small");
-    if (!r && hipMemcpy(out, d_o, got, hipMemcpyDeviceToHost) != hipSuccess) r = fail(BZ2MI_EDEVICE, "D2H copy failed");
-    (void)hipFree(d_o);
-    if (!r) *out_len = got;
-    return r;
+    if ((r = compress_device_impl(c, c->d_in, n, c->d_hout, dcap, &got))) return r;
+    if (got > cap) return fail(BZ2MI_ESPACE, "output buffer too small");
+    if ((r = copy_out_pinned(c, out, c->d_hout, got))) return r;
+    *out_len = got;
+    return BZ2MI_OK;
 }
 
 int bz2mi_compress_device(bz2mi_ctx* c, const void* d_in, size_t n, void* d_out, size_t cap, size_t* out_len,
@@ -863,6 +923,7 @@ int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
         case 2: return bz2mi::mtf_phases(out16);
         case 3: return bz2mi::fe_phases(out16);
         case 4: return bz2mi::tbk_stats(out16);
+        case 5: return bz2mi::tbk_resolve_stats(out16);
         default: return BZ2MI_EINVAL;
     }
 }

@@ -31,6 +31,7 @@ namespace bz2mi {
 
 BZ2MI_PHASE_TABLE(g_bwt_phase)
 BZ2MI_PHASE_TABLE(g_tbk_stat)
+BZ2MI_PHASE_TABLE(g_tbk_res)  // text_resolve sums (PHASES builds)
 #ifdef TBK_TRACE
 __device__ unsigned int* g_tbk_trace;
 #endif
@@ -49,6 +50,15 @@ int tbk_trace(void* p) {
 int tbk_stats(unsigned long long* out) {
 #ifdef BZ2MI_PHASES
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbk_stat), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
+    (void)out;
+    return 0;
+#endif
+}
+
+int tbk_resolve_stats(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbk_res), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
 #else
     (void)out;
     return 0;
@@ -2359,15 +2369,18 @@ __global__ __launch_bounds__(FT) void bwt_block_small_kernel(const uint8_t* __re
 //     T[i-1] = x, in that order (a stable partition by the preceding byte).
 // About half of the rotations of text are placed by the copy step without
 // being sorted.  BWT bytes and origPtr are written as positions become final.
-// Long repeats: rotations still tied after kTextTieCap bytes are not sorted
-// further.  Their SA entries are flagged (kUnres: the run holds the right set
-// of rotations, in an unknown order), the copy steps carry the flag to the
-// rotations they place from them, and after the copy steps the flagged runs
-// are ordered by prefix doubling (Larsson-Sadakane with a depth per group):
-// a group whose rotations share h bytes is sorted on the rank of rotation
-// i + h, where a final rotation's rank is its position and a flagged one's the
-// first position of its group (with the group's depth).  Blocks it cannot
-// finish (periodic blocks, a group larger than kSmall, a full work queue or
+// Long repeats: rotations still tied after kTextTieCap bytes (two-rotation
+// groups: kTextPairCap) are not sorted further in the sort phase.  Their SA
+// entries are flagged (kUnres) and the group goes to a deferred list.  A
+// deferred group of bucket ss is ordered just before ss's copy step, when
+// every bucket processed earlier is complete and its rotations' positions are
+// known (isa): its rotations are compared on their shared text from the
+// group's depth on until they differ or reach a byte c whose bucket is
+// complete, where the positions of rotations i + d in bucket c decide (the
+// order of a pair sharing d bytes is the order of its rotations i + d).  A
+// repeat of ordinary text reaches such a byte within a few bytes, however long
+// the repeat.  Blocks it cannot finish (periodic blocks: no such byte within
+// kDeferScan bytes; a group of more than 64 rotations; a full work queue or
 // pair list) get redo[b] = 2 and go through the general path
 // (bwt_block_kernel mode 1).
 constexpr int kTextDcap = 512;    // depth at which a partition gives up
@@ -2377,15 +2390,14 @@ constexpr int kTextChain = 32;    // levels a partition goes down with one child
 #endif
 constexpr int kTextTieCap = BZ2MI_TEXT_TIECAP;  // tie depth after which a wave sort defers its tied groups
 #ifndef BZ2MI_TEXT_PAIRCAP
-#define BZ2MI_TEXT_PAIRCAP 256
+#define BZ2MI_TEXT_PAIRCAP 64
 #endif
 constexpr int kTextPairCap = BZ2MI_TEXT_PAIRCAP;  // depth to which two tied rotations are compared directly
 constexpr int kTQ = 512;          // work items per round
 constexpr int kCopyR = 4;         // rotations per lane and chunk of a copy step
 constexpr int kTW = 768;          // per-wave LDS words
-constexpr uint32_t kUnres = 0x80000000u;  // SA entry flag: a deferred (unordered) run
-constexpr int kResolveIters = 48;  // doubling rounds before a block is handed back (periodic blocks)
-constexpr uint32_t kDepthMax = 0x7fffu;
+constexpr uint32_t kUnres = 0x80000000u;  // SA entry flag: a member of a deferred group (not yet ordered)
+constexpr uint32_t kDeferScan = 4096;     // bytes a deferred comparison scans before the block goes back
 // non-empty (first, second byte) pairs of a text-path block (~2,000 in a 90 KB
 // block of real text): counted in the per-wave scratch during the setup, and
 // the pair list (uint64 entries) lives in the block's group area, which holds
@@ -2408,7 +2420,8 @@ struct TextLds {
     uint32_t cstart[257];             // first-byte bucket starts
     uint32_t tmp[FW];
     uint32_t wlo[FW], whi[FW];        // a wave's range of pair entries (the deal)
-    uint32_t qn[2], fail, nflag;
+    uint32_t qn[2], fail, nflag, ndef;
+    uint32_t doff[257];               // deferred groups per bucket rank (offsets into the sorted list)
     uint8_t order[256];               // bytes by ascending bucket size
     uint8_t rank[256];                // position of a byte in that order
     uint8_t target[256];
@@ -2519,6 +2532,55 @@ __device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t po
     if (i == 0) *orig = pos;
 }
 
+// Deferred-group entries (a per-block list, capacity n / 2): start (17) |
+// len - 1 (9) | depth (16) | bucket rank (8, set when the list is sorted)
+__device__ __forceinline__ uint64_t dg_make(uint32_t start, uint32_t len, uint32_t depth) {
+    return (uint64_t)start | ((uint64_t)(len - 1) << 17) | ((uint64_t)min(depth, 0xffffu) << 26);
+}
+__device__ __forceinline__ uint32_t dg_start(uint64_t e) { return (uint32_t)e & 0x1ffffu; }
+__device__ __forceinline__ uint32_t dg_len(uint64_t e) { return ((uint32_t)(e >> 17) & 511u) + 1; }
+__device__ __forceinline__ uint32_t dg_depth(uint64_t e) { return (uint32_t)(e >> 26) & 0xffffu; }
+
+// the lanes with `want` append a group (wave-aggregated); a group of more than
+// 64 rotations sends the block back
+__device__ __forceinline__ void dg_push(TextLds& L, uint64_t* dl, bool want, uint32_t start, uint32_t len,
+                                        uint32_t depth) {
+    if (want && len > 64u) atomicOr(&L.fail, 1u);
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&L.ndef, (uint32_t)__popcll(m));
+    base = uniform(base);
+    if (want) dl[base + (uint32_t)__popcll(m & __lanemask_lt())] = dg_make(start, len, depth);
+}
+
+// Order of rotations i0 != i1 that share their first d bytes, when every
+// bucket of rank < s is complete (isa: their positions): -1 if i0 comes first,
+// 1 if i1 does, 0 if no answer within kDeferScan bytes (periodic).
+__device__ __forceinline__ int text_cmp_deferred(const uint8_t* Tl, int n, uint32_t i0, uint32_t i1, uint32_t d,
+                                                 uint32_t s, const uint8_t* rank, const uint32_t* isa) {
+    uint32_t p0 = (i0 + d) % (uint32_t)n, p1 = (i1 + d) % (uint32_t)n;
+    for (uint32_t k = 0; k < kDeferScan; k += 4) {
+        const uint32_t x0 = load4(Tl, n, p0), x1 = load4(Tl, n, p1);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t c0 = (x0 >> (24 - 8 * b)) & 255u, c1 = (x1 >> (24 - 8 * b)) & 255u;
+            if (c0 != c1) return c0 < c1 ? -1 : 1;
+            if (rank[c0] < s) {
+                uint32_t q0 = p0 + b, q1 = p1 + b;
+                if (q0 >= (uint32_t)n) q0 -= (uint32_t)n;
+                if (q1 >= (uint32_t)n) q1 -= (uint32_t)n;
+                return isa[q0] < isa[q1] ? -1 : 1;
+            }
+        }
+        p0 += 4;
+        p1 += 4;
+        if (p0 >= (uint32_t)n) p0 -= (uint32_t)n;
+        if (p1 >= (uint32_t)n) p1 -= (uint32_t)n;
+    }
+    return 0;
+}
+
 // Tied items of a wave sort (W[0, tt): index | slot << 17 | group head << 26,
 // groups in slot order) at depth D: every group of exactly two rotations is
 // ordered by comparing the LDS text directly, 8 bytes at a time, up to
@@ -2526,12 +2588,15 @@ __device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t po
 // or flagged (kUnres) when they still tie there; the items of larger groups
 // are compacted to W[0, return) for another tie round.
 __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_t* sa, uint32_t base, uint32_t tt,
-                                               uint32_t D, uint8_t* out, uint32_t* orig, uint32_t* W, TextLds& L) {
+                                               uint32_t D, uint8_t* out, uint32_t* orig, uint32_t* W, TextLds& L,
+                                               uint64_t* dl) {
     constexpr int E = kSmall / 64;
     const int lane = lane_id();
     uint32_t wv[E];
     bool keep[E], ph[E];
     uint32_t nkeep = 0, nfl = 0;
+    bool dwant[E];
+    uint32_t dst_[E], ddep[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t q = (uint32_t)(lane * E + e);
@@ -2547,6 +2612,9 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int e = 0; e < E; ++e) {
+        dwant[e] = false;
+        dst_[e] = 0;
+        ddep[e] = 0;
         if (!ph[e]) continue;
         const uint32_t q = (uint32_t)(lane * E + e);
         const uint32_t w1 = W[q + 1];
@@ -2555,7 +2623,8 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
         const uint32_t lo = min(s0, s1);
         uint32_t p0 = (i0 + D) % (uint32_t)n, p1 = (i1 + D) % (uint32_t)n;
         int cmp = 0;
-        for (uint32_t dd = D; dd < (uint32_t)kTextPairCap; dd += 8) {
+        uint32_t dd = D;
+        for (; dd < (uint32_t)kTextPairCap; dd += 8) {
             const uint64_t x0 = load8(Tl, n, p0), x1 = load8(Tl, n, p1);
             if (x0 != x1) {
                 cmp = x0 < x1 ? -1 : 1;
@@ -2572,12 +2641,17 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
             sa[base + lo + 1] = c;
             text_final(Tl, n, base + lo, a, out, orig);
             text_final(Tl, n, base + lo + 1, c, out, orig);
-        } else {
+        } else {  // deferred: a group of two sharing dd bytes
             sa[base + lo] = i0 | kUnres;
             sa[base + lo + 1] = i1 | kUnres;
             nfl += 2;
+            dwant[e] = true;
+            dst_[e] = base + lo;
+            ddep[e] = dd;
         }
     }
+#pragma unroll
+    for (int e = 0; e < E; ++e) dg_push(L, dl, dwant[e], dst_[e], 2, ddep[e]);
     const uint32_t nf = wave_sum(nfl);
     if (nf && lane == 0) atomicAdd(&L.nflag, nf);
     const uint32_t inc = wave_incl_sum(nkeep);
@@ -2604,7 +2678,7 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
 #define TBK_PART_INL __forceinline__
 #endif
 __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out, uint32_t* orig,
-                          uint32_t* W, TextLds& L) {
+                          uint32_t* W, TextLds& L, uint64_t* dl) {
     constexpr int E = kSmall / 64;
     const int lane = lane_id();
     TBK_ASSERT(seg.start + seg.len <= (uint32_t)n && seg.len >= 2u && seg.len <= (uint32_t)kSmall, "sort seg", seg.start,
@@ -2627,18 +2701,25 @@ __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, S
     TBK_COUNT(7, seg.len);
     uint32_t D = d + kLdsKeyBytes;
     while (tt) {
-        tt = uniform(text_pairs(Tl, n, sa, seg.start, tt, D, out, orig, W, L));
+        tt = uniform(text_pairs(Tl, n, sa, seg.start, tt, D, out, orig, W, L, dl));
         if (!tt) break;
         TBK_T(8, D << 12 | tt);
         TBK_COUNT(10, 1);
         if (D + kLdsTieBytes > (uint32_t)kTextTieCap) {
-            // deferred: the tied items keep their slots, flagged
+            // deferred: the tied items keep their slots, flagged; every group
+            // (a head item and the items up to the next head, consecutive
+            // slots from the head's) to the deferred list
             for (uint32_t q0 = 0; q0 < tt; q0 += 64) {
                 const uint32_t q = q0 + (uint32_t)lane;
-                if (q < tt) {
-                    const uint32_t w = W[q];
-                    sa[seg.start + ((w >> 17) & 511u)] = (w & 0x1ffffu) | kUnres;
+                const uint32_t w = q < tt ? W[q] : 0u;
+                if (q < tt) sa[seg.start + ((w >> 17) & 511u)] = (w & 0x1ffffu) | kUnres;
+                uint32_t glen = 0;
+                const bool hd = q < tt && (w >> 26);
+                if (hd) {
+                    glen = 1;
+                    while (q + glen < tt && !(W[q + glen] >> 26)) ++glen;
                 }
+                dg_push(L, dl, hd, seg.start + ((w >> 17) & 511u), glen, D);
             }
             if (lane == 0) atomicAdd(&L.nflag, tt);
             return;
@@ -2664,9 +2745,8 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     uint32_t c[4];
     const uint32_t dcap = min((uint32_t)kTextDcap, d + (uint32_t)kTextChain);
     for (;;) {
-        if (d >= dcap) {
-            for (uint32_t k = lane; k < seg.len; k += 64) sa[seg.start + k] = ld_fresh(sa + seg.start + k) | kUnres;
-            if (lane == 0) atomicAdd(&L.nflag, seg.len);
+        if (d >= dcap) {  // more than kSmall rotations sharing d bytes: the general path
+            if (lane == 0) atomicOr(&L.fail, 1u);
             return;
         }
         TBK_COUNT(5, 1);
@@ -2761,253 +2841,60 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     __builtin_amdgcn_wave_barrier();
 }
 
-// common prefix length of rotations i and j, capped at `cap` (a multiple of 8)
-__device__ __forceinline__ uint32_t text_lcp(const uint8_t* Tl, int n, uint32_t i, uint32_t j, uint32_t cap) {
-    uint32_t l = 0;
-    uint32_t pi = i, pj = j;
-    while (l < cap) {
-        const uint64_t x = load8(Tl, n, pi) ^ load8(Tl, n, pj);
-        if (x) return l + ((uint32_t)__builtin_clzll(x) >> 3);
-        l += 8;
-        pi += 8;
-        pj += 8;
-        if (pi >= (uint32_t)n) pi -= (uint32_t)n;
-        if (pj >= (uint32_t)n) pj -= (uint32_t)n;
-    }
-    return cap;
-}
-
-// Rank word of a rotation during the resolve: position << 15 | depth, where
-// a final rotation has its own position and depth 0 and a flagged one the
-// first position of its group and the group's depth (a lower bound of the
-// common prefix of its rotations, >= 2).  Sorting rank words sorts by
-// position.
-__device__ __forceinline__ uint32_t rw_make(uint32_t pos, uint32_t depth) { return (pos << 15) | depth; }
-
-// resolve: one group of 3..kSmall rotations at `head` sorted by its keys (one wave)
-template <int E>
-__device__ __forceinline__ void resolve_wave(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa,
-                                             const uint32_t* key, uint8_t* out, uint32_t* orig, uint32_t head,
-                                             uint32_t m, uint32_t depth, uint32_t* W, TextLds& L, uint32_t* gnext,
-                                             int nxt) {
-    const int lane = lane_id();
-    uint64_t k[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t g = (uint32_t)(e * 64 + lane);
-        k[e] = g < m ? ((uint64_t)ld_fresh(key + head + g) << 32) | (ld_fresh(sa + head + g) & 0x1ffffu) : ~0ull;
-    }
-    uint32_t dummy[E];
-    wave_bitonic<E, false>(k, dummy);
-    // sorted: item r = lane * E + e
-    const uint32_t pk = lane_prev((uint32_t)(k[E - 1] >> 32), 0u);
-    bool hd[E];
-    uint32_t run = 0;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t r = (uint32_t)lane * E + e;
-        const uint32_t kw = (uint32_t)(k[e] >> 32);
-        const uint32_t prev = e ? (uint32_t)(k[e - 1] >> 32) : pk;
-        hd[e] = r < m && (r == 0 || kw != prev);
-        if (hd[e]) run = r;
-        if (r < m) W[r] = hd[e] ? 1u : 0u;
-    }
-    if (lane == 0) W[m] = 1u;
-    const uint32_t carry = lane_prev(wave_incl_max(run), 0u);
-    __builtin_amdgcn_wave_barrier();
-    uint32_t cur = carry;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t r = (uint32_t)lane * E + e;
-        if (hd[e]) cur = r;
-        bool want = false;
-        uint32_t glen = 0;
-        if (r < m) {
-            const uint32_t i = (uint32_t)k[e] & 0x1ffffu, kw = (uint32_t)(k[e] >> 32);
-            const uint32_t pos = head + r;
-            const bool single = hd[e] && W[r + 1];
-            if (single) {
-                sa[pos] = i;
-                isa[i] = rw_make(pos, 0);
-                text_final(Tl, n, pos, i, out, orig);
-            } else {
-                const uint32_t nd = min(depth + (kw & kDepthMax), kDepthMax);
-                sa[pos] = i | kUnres;
-                isa[i] = rw_make(head + cur, nd);
-                if (hd[e]) {
-                    glen = 1;
-                    while (!W[r + glen]) ++glen;
-                    want = true;
-                }
-            }
-        }
-        const uint64_t mm = __ballot(want);
-        if (mm) {
-            uint32_t b0 = 0;
-            if (lane == 0) b0 = atomicAdd(&L.qn[nxt], (uint32_t)__popcll(mm));
-            b0 = uniform(b0);
-            if (want) gnext[b0 + (uint32_t)__popcll(mm & __lanemask_lt())] = (head + r) | ((glen - 1) << 17);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
-// Order the flagged runs (the whole workgroup, after the copy steps): groups
-// are the flagged runs split where the first two bytes change, each with the
-// common prefix of its rotations (min of neighbour LCPs, capped); then rounds
-// of doubling until no group is left.  isa: n words, key: n words, glist:
-// two lists of n/2 + 1 words.  Returns false when the block has to go back.
-__device__ void text_resolve(const uint8_t* Tl, int n, uint32_t* __restrict__ sa, uint32_t* __restrict__ isa,
-                             uint32_t* __restrict__ key, uint32_t* __restrict__ glist, uint8_t* __restrict__ out,
-                             uint32_t* orig, TextLds& L) {
-    const int t = threadIdx.x, w = wave_id();
-    uint32_t* W = L.w[w];
-    uint32_t* gl[2] = {glist, glist + ((uint32_t)n / 2 + 1)};
-    if (t == 0) L.qn[0] = 0;
-    __syncthreads();
-    for (uint32_t k = t; k < (uint32_t)n; k += FT) {
-        const uint32_t v = ld_fresh(sa + k), i = v & 0x1ffffu;
-        if (!(v & kUnres)) {
-            isa[i] = rw_make(k, 0);
-            continue;
-        }
-        const uint32_t pi = ((uint32_t)Tl[i] << 8) | Tl[i + 1 < (uint32_t)n ? i + 1 : 0u];
-        bool head = k == 0;
-        if (!head) {
-            const uint32_t u = ld_fresh(sa + k - 1), iu = u & 0x1ffffu;
-            head = !(u & kUnres) || (((uint32_t)Tl[iu] << 8) | Tl[iu + 1 < (uint32_t)n ? iu + 1 : 0u]) != pi;
-        }
-        if (!head) continue;
-        uint32_t len = 1, dep = (uint32_t)kTextPairCap & ~7u, prev = i;
-        while (k + len < (uint32_t)n) {
-            const uint32_t u = ld_fresh(sa + k + len), iu = u & 0x1ffffu;
-            if (!(u & kUnres) || (((uint32_t)Tl[iu] << 8) | Tl[iu + 1 < (uint32_t)n ? iu + 1 : 0u]) != pi) break;
-            dep = min(dep, text_lcp(Tl, n, prev, iu, dep));
-            prev = iu;
-            if (++len > (uint32_t)kSmall) break;
-        }
-        if (len > (uint32_t)kSmall) {
+// The deferred groups of bucket rank s (sorted list dl2[doff[s], doff[s+1])),
+// ordered with text_cmp_deferred: groups of two one per thread, larger ones
+// (up to 64) one per wave, every member ranked by comparing it with the
+// others.  Final SA entries, BWT bytes, origPtr and isa.
+__device__ void text_resolve_rank(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa, const uint64_t* dl2,
+                                  uint32_t s, uint8_t* out, uint32_t* orig, TextLds& L) {
+    const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+    const uint32_t g0 = L.doff[s], g1 = L.doff[s + 1];
+    for (uint32_t g = g0 + (uint32_t)t; g < g1; g += FT) {
+        const uint64_t e = dl2[g];
+        if (dg_len(e) != 2) continue;
+        const uint32_t st = dg_start(e);
+        const uint32_t i0 = ld_fresh(sa + st) & 0x1ffffu, i1 = ld_fresh(sa + st + 1) & 0x1ffffu;
+        const int c = text_cmp_deferred(Tl, n, i0, i1, dg_depth(e), s, L.rank, isa);
+        if (c == 0) {
             atomicOr(&L.fail, 1u);
             continue;
         }
-        if (len == 1) {
-            sa[k] = i;
-            isa[i] = rw_make(k, 0);
-            text_final(Tl, n, k, i, out, orig);
-            continue;
-        }
-        dep = max(dep, 2u);
-        for (uint32_t j = 0; j < len; ++j) isa[ld_fresh(sa + k + j) & 0x1ffffu] = rw_make(k, dep);
-        gl[0][atomicAdd(&L.qn[0], 1u)] = k | ((len - 1) << 17);
+        const uint32_t a = c < 0 ? i0 : i1, b = c < 0 ? i1 : i0;
+        sa[st] = a;
+        sa[st + 1] = b;
+        isa[a] = st;
+        isa[b] = st + 1;
+        text_final(Tl, n, st, a, out, orig);
+        text_final(Tl, n, st + 1, b, out, orig);
     }
-    __threadfence_block();
-    __syncthreads();
-    for (int it = 0, cur = 0;; ++it, cur ^= 1) {
-        const uint32_t ng = uniform(L.qn[cur]);
-        if (ng == 0 || uniform(L.fail)) break;
-        if (it >= kResolveIters) {
-            if (t == 0) L.fail = 1u;
-            break;
-        }
-        __syncthreads();  // every thread has read the count
-        if (t == 0) L.qn[cur ^ 1] = 0;
-        const uint32_t* ga = gl[cur];
-        // keys: the rank word of rotation i + depth, for every member (a
-        // snapshot).  Groups of two (nearly all: repeats tie in pairs) U at a
-        // time per thread with their loads in flight together; larger groups
-        // one member at a time.
-        constexpr int U = 4;
-        for (uint32_t g0 = t; g0 < ng; g0 += FT * U) {
-            uint32_t e[U], v0[U], v1[U], dp[U], k0[U], k1[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t g = g0 + (uint32_t)u * FT;
-                e[u] = g < ng ? ga[g] : 0xffffffffu;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t head = e[u] & 0x1ffffu;
-                v0[u] = e[u] != 0xffffffffu ? sa[head] & 0x1ffffu : 0u;
-                v1[u] = e[u] != 0xffffffffu ? sa[head + 1] & 0x1ffffu : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) dp[u] = e[u] != 0xffffffffu ? isa[v0[u]] & kDepthMax : 0u;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                k0[u] = e[u] != 0xffffffffu ? isa[(v0[u] + dp[u]) % (uint32_t)n] : 0u;
-                k1[u] = e[u] != 0xffffffffu ? isa[(v1[u] + dp[u]) % (uint32_t)n] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (e[u] == 0xffffffffu) continue;
-                const uint32_t head = e[u] & 0x1ffffu, len = (e[u] >> 17) + 1;
-                key[head] = k0[u];
-                key[head + 1] = k1[u];
-                for (uint32_t j = 2; j < len; ++j)
-                    key[head + j] = isa[((sa[head + j] & 0x1ffffu) + dp[u]) % (uint32_t)n];
-            }
-        }
-        __threadfence_block();
-        __syncthreads();
-        // pairs: one thread each, U at a time
-        for (uint32_t g0 = t; g0 < ng; g0 += FT * U) {
-            uint32_t e[U], v0[U], v1[U], k0[U], k1[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t g = g0 + (uint32_t)u * FT;
-                const uint32_t x = g < ng ? ga[g] : 0xffffffffu;
-                e[u] = (x != 0xffffffffu && (x >> 17) == 1u) ? x : 0xffffffffu;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t head = e[u] & 0x1ffffu;
-                const bool ok = e[u] != 0xffffffffu;
-                v0[u] = ok ? sa[head] & 0x1ffffu : 0u;
-                v1[u] = ok ? sa[head + 1] & 0x1ffffu : 0u;
-                k0[u] = ok ? key[head] : 0u;
-                k1[u] = ok ? key[head + 1] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (e[u] == 0xffffffffu) continue;
-                const uint32_t head = e[u] & 0x1ffffu;
-                const uint32_t i0 = v0[u], i1 = v1[u];
-                if (k0[u] == k1[u]) {
-                    const uint32_t dep = isa[i0] & kDepthMax;
-                    const uint32_t nd = min(dep + (k0[u] & kDepthMax), kDepthMax);
-                    isa[i0] = rw_make(head, nd);
-                    isa[i1] = rw_make(head, nd);
-                    gl[cur ^ 1][atomicAdd(&L.qn[cur ^ 1], 1u)] = e[u];
-                } else {
-                    const bool sw = k1[u] < k0[u];
-                    const uint32_t a = sw ? i1 : i0, c = sw ? i0 : i1;
-                    sa[head] = a;
-                    sa[head + 1] = c;
-                    isa[a] = rw_make(head, 0);
-                    isa[c] = rw_make(head + 1, 0);
-                    text_final(Tl, n, head, a, out, orig);
-                    text_final(Tl, n, head + 1, c, out, orig);
+    for (uint32_t gb = g0 + (uint32_t)w * 64; gb < g1; gb += FT) {
+        const uint32_t g = gb + (uint32_t)lane;
+        const uint64_t e = g < g1 ? dl2[g] : 0ull;
+        for (uint64_t mm = __ballot(g < g1 && dg_len(e) > 2); mm; mm &= mm - 1) {
+            const int l = __builtin_ctzll(mm);
+            const uint32_t lo = uniform((uint32_t)__shfl((int)(uint32_t)e, l));
+            const uint32_t hi = uniform((uint32_t)__shfl((int)(uint32_t)(e >> 32), l));
+            const uint64_t ee = ((uint64_t)hi << 32) | lo;
+            const uint32_t st = dg_start(ee), m = dg_len(ee), dep = dg_depth(ee);
+            const uint32_t me = (uint32_t)lane < m ? ld_fresh(sa + st + lane) & 0x1ffffu : 0u;
+            uint32_t below = 0;
+            bool bad = false;
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint32_t other = (uint32_t)__shfl((int)me, (int)k);
+                if ((uint32_t)lane < m && k != (uint32_t)lane) {
+                    const int c = text_cmp_deferred(Tl, n, other, me, dep, s, L.rank, isa);
+                    below += c < 0 ? 1u : 0u;
+                    bad |= c == 0;
                 }
             }
-        }
-        // larger groups: one wave each (chunks of 64 list entries dealt to the waves)
-        for (uint32_t g0 = (uint32_t)w * 64; g0 < ng; g0 += FT) {
-            const uint32_t g = g0 + (uint32_t)lane_id();
-            const uint32_t e = g < ng ? ld_fresh(ga + g) : 0u;
-            const uint32_t len = (e >> 17) + 1;
-            for (uint64_t mm = __ballot(g < ng && len > 2); mm; mm &= mm - 1) {
-                const int l = __builtin_ctzll(mm);
-                const uint32_t ee = uniform((uint32_t)__shfl((int)e, l));
-                const uint32_t head = ee & 0x1ffffu, m = (ee >> 17) + 1;
-                const uint32_t dep = uniform(ld_fresh(isa + (ld_fresh(sa + head) & 0x1ffffu)) & kDepthMax);
-                if (m <= 64) resolve_wave<1>(Tl, n, sa, isa, key, out, orig, head, m, dep, W, L, gl[cur ^ 1], cur ^ 1);
-                else if (m <= 128) resolve_wave<2>(Tl, n, sa, isa, key, out, orig, head, m, dep, W, L, gl[cur ^ 1], cur ^ 1);
-                else if (m <= 256) resolve_wave<4>(Tl, n, sa, isa, key, out, orig, head, m, dep, W, L, gl[cur ^ 1], cur ^ 1);
-                else resolve_wave<8>(Tl, n, sa, isa, key, out, orig, head, m, dep, W, L, gl[cur ^ 1], cur ^ 1);
+            if (__ballot(bad) && lane == 0) atomicOr(&L.fail, 1u);
+            __builtin_amdgcn_wave_barrier();  // every lane has read its member before the writes
+            if ((uint32_t)lane < m) {
+                sa[st + below] = me;
+                isa[me] = st + below;
+                text_final(Tl, n, st + below, me, out, orig);
             }
         }
-        __threadfence_block();
-        __syncthreads();
     }
 }
 
@@ -3034,6 +2921,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     uint32_t* spill = spill_all + (size_t)b * stride;
     // the pair list (kPairCap entries at most; a block with more goes back)
     uint64_t* pl = reinterpret_cast<uint64_t*>(grp_all + (size_t)b * bwt_group_stride(stride));
+    // deferred groups (n / 2 at most) as found, then sorted by bucket rank
+    uint64_t* dl = key_all + (size_t)b * tcap;
+    uint64_t* dl2 = glist_all + (size_t)b * tcap;
     const uint8_t* Tl = reinterpret_cast<const uint8_t*>(L.text);
     uint32_t* W = L.w[w];
     {
@@ -3054,6 +2944,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     if (t == 0) {
         L.fail = 0;
         L.nflag = 0;
+        L.ndef = 0;
     }
     if (t < FW) {
         L.wlo[t] = 0xffffffffu;
@@ -3203,7 +3094,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
                 const unsigned long long ti0 = wall_clock64();
 #endif
-                if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, 2, out, orig, W, L);
+                if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, 2, out, orig, W, L, dl);
                 else text_partition(Tl, n, sa, spill, seg, 2, out, orig, W, L, 0);
                 TBK_T(10, seg.len);
 #ifdef BZ2MI_PHASES
@@ -3254,7 +3145,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
             const unsigned long long ti0 = wall_clock64();
 #endif
-            if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, d, out, orig, W, L);
+            if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, d, out, orig, W, L, dl);
             else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, cur ^ 1);
             TBK_T(11, seg.len);
 #ifdef BZ2MI_PHASES
@@ -3268,6 +3159,51 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     __syncthreads();
 #ifdef BZ2MI_PHASES
     tks = wall_clock64() - tk1;
+#endif
+    // ---- deferred groups: isa (the position of every final rotation so far,
+    // in spill: free after the sort phase), the groups sorted by the rank of
+    // their bucket, then the groups of the buckets sorted whole (ranks before
+    // s_big) ordered in ascending rank -- each sees every earlier bucket
+    // complete
+    const uint32_t ndef = uniform(L.ndef);
+    const bool need_isa = ndef != 0 && !uniform(L.fail);
+    uint32_t* isa = spill;
+#ifdef BZ2MI_PHASES
+    unsigned long long tkr = wall_clock64();
+#endif
+    if (need_isa) {
+        for (uint32_t k = t; k < (uint32_t)n; k += FT) {
+            const uint32_t v = ld_fresh(sa + k);
+            if (!(v & kUnres)) isa[v] = k;
+        }
+        if (t < 257) L.doff[t] = 0;
+        __syncthreads();
+        for (uint32_t g = t; g < ndef; g += FT)
+            atomicAdd(&L.doff[L.rank[Tl[ld_fresh(sa + dg_start(dl[g])) & 0x1ffffu]]], 1u);
+        __syncthreads();
+        uint32_t tot;
+        const uint32_t ex = wg_excl_sum<FT>(t < 256 ? L.doff[t] : 0u, L.tmp, &tot);
+        if (t < 256) {
+            L.doff[t] = ex;
+            L.pcol[t] = ex;
+        }
+        if (t == 0) L.doff[256] = tot;
+        __syncthreads();
+        for (uint32_t g = t; g < ndef; g += FT) {
+            const uint64_t e = dl[g];
+            dl2[atomicAdd(&L.pcol[L.rank[Tl[ld_fresh(sa + dg_start(e)) & 0x1ffffu]]], 1u)] = e;
+        }
+        __threadfence_block();
+        __syncthreads();
+        for (uint32_t s = s0; s < s_big; ++s) {
+            if (L.doff[s + 1] == L.doff[s]) continue;  // (uniform: LDS after a barrier)
+            text_resolve_rank(Tl, n, sa, isa, dl2, s, out, orig, L);
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
+#ifdef BZ2MI_PHASES
+    tkr = wall_clock64() - tkr;
 #endif
     // ---- copy steps.  The pair starts go to LDS (the per-wave scratch is
     // free now: 16 x 256 copy counters, then the starts).
@@ -3307,7 +3243,8 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                 const uint64_t peers = wave_match8(x, tgt);
                 if (tgt) {
                     const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
-                    sa[bs + below] = j | (v & kUnres);
+                    sa[bs + below] = j;
+                    if (need_isa) isa[j] = bs + below;
                     text_final(Tl, n, bs + below, j, out, orig);
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -3327,6 +3264,18 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
         tk1 = wall_clock64();
 #endif
+        if (need_isa && L.doff[s + 1] > L.doff[s]) {  // bucket ss's deferred groups first
+#ifdef BZ2MI_PHASES
+            const unsigned long long tr0 = wall_clock64();
+#endif
+            text_resolve_rank(Tl, n, sa, isa, dl2, s, out, orig, L);
+            __threadfence_block();
+            __syncthreads();
+#ifdef BZ2MI_PHASES
+            tkr += wall_clock64() - tr0;
+#endif
+            if (uniform(L.fail)) break;
+        }
         bool tg = false;
         if (t < 256) {
             const uint32_t x = (uint32_t)t, wq = ss >> 5, bit = ss & 31u;
@@ -3363,11 +3312,11 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #pragma unroll
                 for (int r = 0; r < kCopyR; ++r) {
                     const bool v = jv[r] != 0xffffffffu;
-                    const uint32_t i = jv[r] & 0x1ffffu;
+                    const uint32_t i = jv[r];
                     const uint32_t j = i ? i - 1 : (uint32_t)n - 1;
                     const uint32_t x = v ? (uint32_t)Tl[j] : 0u;
                     const bool tgt = v && L.target[x];
-                    jv[r] = j | (jv[r] & kUnres);
+                    jv[r] = j;
                     xv[r] = tgt ? x : 0x100u;
                     if (tgt) atomicAdd(&C[x], 1u);
                 }
@@ -3393,7 +3342,8 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                         const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
                         const uint32_t pos = bs + below;
                         sa[pos] = jv[r];
-                        text_final(Tl, n, pos, jv[r] & 0x1ffffu, out, orig);
+                        if (need_isa) isa[jv[r]] = pos;
+                        text_final(Tl, n, pos, jv[r], out, orig);
                         if (below == 0) C[x] = bs + (uint32_t)__popcll(peers);
                     }
                     __builtin_amdgcn_wave_barrier();
@@ -3406,18 +3356,6 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         tkc += wall_clock64() - tk1;
 #endif
     }
-    // ---- deferred runs (long repeats): prefix doubling over the flagged runs
-#ifdef BZ2MI_PHASES
-    const unsigned long long tkr0 = wall_clock64();
-#endif
-    if (!failed && uniform(L.nflag)) {
-        uint32_t* key = reinterpret_cast<uint32_t*>(key_all + (size_t)b * tcap);
-        uint32_t* glist = reinterpret_cast<uint32_t*>(glist_all + (size_t)b * tcap);
-        text_resolve(Tl, n, sa, spill, key, glist, out, orig, L);
-    }
-#ifdef BZ2MI_PHASES
-    const unsigned long long tkr = wall_clock64() - tkr0;
-#endif
     __syncthreads();
     if (t == 0 && L.fail) redo[b] = 2u;
     TBK_T(6, L.fail);
@@ -3429,6 +3367,11 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         atomicAdd(&g_tbk_stat[9], wall_clock64() - tk0);
         atomicAdd(&g_tbk_stat[11], (unsigned long long)L.nflag);
         atomicAdd(&g_tbk_stat[14], tkr);
+        if (ndef) {
+            atomicAdd(&g_tbk_res[8], 1ull);
+            atomicAdd(&g_tbk_res[2], (unsigned long long)ndef);
+            atomicMax(&g_tbk_res[9], (unsigned long long)ndef);
+        }
         atomicMax(&g_tbk_stat[15], wall_clock64() - tk0);
         for (int k = 3; k < 8; ++k) atomicAdd(&g_tbk_stat[k], (unsigned long long)L.stat[k]);
         for (int k = 10; k < 14; ++k)

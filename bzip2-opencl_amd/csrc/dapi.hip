@@ -36,6 +36,10 @@ const char* dec_message(uint32_t status) {
     }
 }
 
+// set by grow() when the device was out of memory: run_decode retries the
+// window with smaller budgets
+thread_local bool g_dec_oom = false;
+
 template <class T>
 int grow(T** p, size_t* cap, size_t count) {
     if (count <= *cap && *p) return BZ2MI_OK;
@@ -44,7 +48,13 @@ int grow(T** p, size_t* cap, size_t count) {
     *cap = 0;
     const size_t c = std::max<size_t>(count, 1);
     hipError_t e = hipMalloc((void**)p, c * sizeof(T));
-    if (e != hipSuccess) return bz2mi_set_error(BZ2MI_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+    if (e != hipSuccess) {
+        if (e == hipErrorOutOfMemory) {
+            g_dec_oom = true;
+            (void)hipGetLastError();  // not sticky: the retry may allocate less
+        }
+        return bz2mi_set_error(BZ2MI_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
     *cap = c;
     return BZ2MI_OK;
 }
@@ -64,6 +74,7 @@ struct DecWalk {
 
 struct bz2mi_dctx {
     int unit = 10000, device = 0, cus = 256;
+    uint64_t trailing = 0;  // input bytes after the last decoded stream (ignored)
     int flags = 0;  // BZ2MI_DEC_CONCATENATED: every stream of the input (bzip2), else the first (reference)
     hipStream_t stream = nullptr;
     uint32_t* d_crctab = nullptr;
@@ -114,15 +125,11 @@ struct bz2mi_dctx {
 
 namespace {
 
-// inverse-BWT workgroups per XCD (BZ2MI_IBWT_XCD overrides, for experiments)
-int ibwt_wg_per_xcd() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("BZ2MI_IBWT_XCD");
-        v = (e && atoi(e) > 0) ? atoi(e) : 32;  // measured 8/16/24/32: 101/64/55/58 ms per GiB random, 100/59/45/42 text
-    }
-    return v;
-}
+// inverse-BWT workgroups per XCD (A/B builds: -DBZ2MI_AB_IBWT_XCD=n)
+#ifndef BZ2MI_AB_IBWT_XCD
+#define BZ2MI_AB_IBWT_XCD 32  // measured 8/16/24/32: 101/64/55/58 ms per GiB random, 100/59/45/42 text
+#endif
+constexpr int ibwt_wg_per_xcd() { return BZ2MI_AB_IBWT_XCD; }
 
 // an element of the stream in order: a header, a block, an end marker
 struct DecEvent {
@@ -478,7 +485,7 @@ int run_window(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint64_t start, boo
             // (an inconsistent BWT -- `bad` -- yields garbage bytes: the reference
             // would find the same CRC mismatch)
             // (count mode writes nothing and computes no CRCs: sizes only)
-            if (!count_only && (bad[bi] || crc[bi] != e.val) && !getenv("BZ2MI_DNOCRC")) {
+            if (!count_only && (bad[bi] || crc[bi] != e.val)) {
                 res->end_bit = e.pos;
                 res->out_len = ooff[bi];
                 res->err = BZ2MI_EFORMAT;
@@ -518,14 +525,21 @@ int run_window(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint64_t start, boo
 
 // Candidates one window may decode: symbols for max(64 x input, 1 GiB) of
 // memory (a legitimate stream is one window: a block's symbols and stage
-// vectors are ~12 bytes per decoded byte; BZ2MI_DEC_BUDGET overrides), tables
-// for as many candidates or 2 x the input, whichever is more (a crafted input
-// of magic matches everywhere costs tables for that many, not per match).
+// vectors are ~12 bytes per decoded byte), capped at half the device's free
+// memory and kDecBudgetMax so the budget bounds memory whatever the input
+// size (a larger stream is decoded in several windows; BZ2MI_DEC_BUDGET sets
+// the budget), tables for as many candidates or 2 x the input, whichever is
+// more (a crafted input of magic matches everywhere costs tables for that
+// many, not per match).
+constexpr size_t kDecBudgetMax = (size_t)32 << 30;
 void window_kmax(const bz2mi_dctx* d, size_t n, size_t* kmax_c, size_t* kmax_s) {
     size_t budget = std::max<size_t>((size_t)64 * n, (size_t)1 << 30);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr) budget = std::min(budget, fr / 2);
+    budget = std::min(budget, kDecBudgetMax);
     if (const char* e = getenv("BZ2MI_DEC_BUDGET")) budget = (size_t)strtoull(e, nullptr, 10);
     *kmax_s = std::max<size_t>(64, budget / symbol_bytes(d->unit));
-    *kmax_c = std::max<size_t>(*kmax_s, 2 * n / table_bytes());
+    *kmax_c = std::max<size_t>(*kmax_s, std::min<size_t>(2 * n, budget) / table_bytes());
 }
 
 // the whole decode of n bytes at d_in (4-byte aligned) into d_out: windows
@@ -534,6 +548,7 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
                hipStream_t s) {
     *out_len = 0;
     d->walk = DecWalk{};
+    d->trailing = 0;
     for (float& m : d->ms) m = 0.f;
     size_t kmax_c, kmax_s;
     window_kmax(d, n, &kmax_c, &kmax_s);
@@ -552,11 +567,23 @@ int run_decode(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint8_t* d_out, siz
             counting = true;
             continue;  // (the walk state is unchanged by a call that fails this way)
         }
+        if (r == BZ2MI_EDEVICE && g_dec_oom && kmax_s > 64) {
+            // out of device memory while sizing this window's buffers (before
+            // the walk moves): the same window again with half the budgets
+            g_dec_oom = false;
+            kmax_s = std::max<size_t>(64, kmax_s / 2);
+            kmax_c = std::max<size_t>(kmax_s, kmax_c / 2);
+            continue;
+        }
+        g_dec_oom = false;
         if (r != BZ2MI_OK) return r;
         total += res.out_len;
         if (res.err != BZ2MI_OK) return bz2mi_set_error(res.err, res.msg);
         const uint64_t next = (uint64_t)wb * 8 + res.end_bit;
-        if (res.done) break;
+        if (res.done) {
+            d->trailing = n - std::min<uint64_t>(n, (next + 7) / 8);
+            break;
+        }
         if (next == bit && res.out_len == 0) return bz2mi_set_error(BZ2MI_EFORMAT, "BZip2 stream format error");
         bit = next;
     }
@@ -725,6 +752,12 @@ int bz2mi_dstream(bz2mi_dctx* d, const uint8_t* in, size_t n, unsigned start_bit
 int bz2mi_dset_flags(bz2mi_dctx* d, int flags) {
     if (!d || (flags & ~BZ2MI_DEC_CONCATENATED)) return bz2mi_set_error(BZ2MI_EINVAL, "invalid decoder flags");
     d->flags = flags;
+    return BZ2MI_OK;
+}
+
+int bz2mi_dlast_trailing(bz2mi_dctx* d, uint64_t* bytes) {
+    if (!d || !bytes) return bz2mi_set_error(BZ2MI_EINVAL, "null argument");
+    *bytes = d->trailing;
     return BZ2MI_OK;
 }
 

@@ -150,6 +150,12 @@ struct bz2mi_ctx {
     bz2mi::host::FrontBufs fe;
     uint8_t* d_in = nullptr;        // staging for host input
     size_t in_cap = 0;
+    // bz2mi_compress (host bytes): the stream in HBM, kept across calls, and
+    // two pinned staging buffers the copies are pipelined through
+    uint8_t* d_hout = nullptr;
+    size_t hout_cap = 0;
+    uint8_t* h_pin[2] = {nullptr, nullptr};
+    hipEvent_t ev_pin[2] = {nullptr, nullptr};
     hipEvent_t ev[8] = {};
     hipEvent_t ev_in = nullptr;  // caller stream -> context stream hand-off
     std::vector<hipEvent_t> tev;  // per-batch stage timing events (12 per batch)

@@ -104,6 +104,7 @@ int bwt_phases(unsigned long long* out);
 int mtf_phases(unsigned long long* out);
 int fe_phases(unsigned long long* out);
 int tbk_stats(unsigned long long* out);
+int tbk_resolve_stats(unsigned long long* out);
 int tbk_trace(void* host_mapped);
 int run_selftest(uint32_t* host_bad, int n);  // cross-lane primitive checks
 int huffman_threads();  // workgroup size of huffman_kernel

@@ -448,11 +448,13 @@ void launch_mtf(int nb, const uint8_t* bwt, size_t stride, const uint32_t* lens,
     // waves per block: one while the blocks alone fill the chip's SIMDs
     // several times over (each wave's tile chain is latency-bound below ~6
     // waves per SIMD), else segments
-    static const int force = [] {
-        const char* e = getenv("BZ2MI_MTF_WAVES");  // A/B override: 1, 2, 4 or 8
-        return e ? atoi(e) : 0;
-    }();
-    const int g = force ? force : nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : 8;
+    // (every instance runs in the tests: 1 GiB batches take G = 1, the 900 KB
+    // mode and small batches 4 / 8; A/B builds: -DBZ2MI_AB_MTF_WAVES=G)
+#ifdef BZ2MI_AB_MTF_WAVES
+    const int g = BZ2MI_AB_MTF_WAVES;
+#else
+    const int g = nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : 8;
+#endif
 #define BZ2MI_MTF_LAUNCH(G)                                                                                     \
     hipLaunchKernelGGL(mtf_kernel<G>, dim3(nb), dim3(64 * G), 0, s, bwt, stride, lens, nb, present, mtf_out,      \
                        mtf_stride, mtf_len, alpha_out, hist_out, scratch, scratch_stride)

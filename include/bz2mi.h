@@ -39,6 +39,12 @@ const char* bz2mi_last_error(void);
 /* Library / device information. */
 int bz2mi_device_count(void);
 const char* bz2mi_version(void);
+/* ABI revision of this header's entry points: a host checks it at load time.
+ *   3: bz2mi_unit_assemble / _host gained the trailing hip_stream argument;
+ *      bz2mi_decompress* decode the first stream only (the reference)
+ *   4: bz2mi_dlast_trailing, bz2mi_abi_version */
+#define BZ2MI_ABI_VERSION 4
+int bz2mi_abi_version(void);
 
 /*
  * Create a compression context on HIP device `device`.
@@ -244,6 +250,11 @@ int bz2mi_decompress_device(bz2mi_dctx* d, const void* d_in, size_t n, void* d_o
 int bz2mi_dstream_reset(bz2mi_dctx* d);
 int bz2mi_dstream(bz2mi_dctx* d, const uint8_t* in, size_t n, unsigned start_bit, int final, uint8_t* out,
                   size_t cap, uint64_t* end_bit, size_t* out_len, int* done);
+
+/* bytes of the last bz2mi_decompress* input after the end of the last
+ * stream it decoded (ignored, as by the reference's InputStream, which reads
+ * the first stream; with BZ2MI_DEC_CONCATENATED: bytes that start no stream) */
+int bz2mi_dlast_trailing(bz2mi_dctx* d, uint64_t* bytes);
 
 /* milliseconds of the last call: [0] candidate scan, [1] Huffman symbols,
  * [2] MTF + RLE2 (and the stream walk), [3] inverse BWT, [4] RLE1 + CRC, [5] whole call */

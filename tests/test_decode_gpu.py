@@ -44,6 +44,8 @@ def _inputs():
     yield "empty", b""
     yield "one", b"x"
     yield "text", synth.text_bytes(3 << 20).tobytes()
+    yield "realtext", synth.realtext_bytes(3 << 20).tobytes()
+    yield "repeats", synth.repeats_bytes(2 << 20).tobytes()
     yield "random", synth.random_bytes(3 << 20).tobytes()
     yield "runs", synth.runs_bytes(3 << 20).tobytes()
     yield "runs_long", synth.runs_bytes(2 << 20, max_run=5000).tobytes()
@@ -73,6 +75,18 @@ def test_stock_bzip2_files_need_unit_100000(bz):
     # (the message its probe saw)
     with bz.Decompressor(10000) as d, pytest.raises(bz.DecompressError, match="block Huffman tables invalid"):
         d.decompress(z)
+
+
+def test_decode_budget_smaller_than_the_stream(bz, monkeypatch):
+    """A symbol budget (BZ2MI_DEC_BUDGET) far below the stream's decoded size:
+    the stream is decoded in many windows with the same bytes (the
+    budget bounds device memory whatever the input size)."""
+    from bz2mi import synth
+    data = synth.mixed_bytes(24 << 20, segment=2 << 20).tobytes()
+    z = bz.compress(data, 9, 10)
+    monkeypatch.setenv("BZ2MI_DEC_BUDGET", str(16 << 20))  # ~16 blocks per window of ~270
+    with bz.Decompressor(10000) as d:
+        assert d.decompress(z) == data
 
 
 def test_900k_mode_round_trip(bz):

@@ -33,4 +33,8 @@ print(f"  sorts {v[4] / nb:.1f} ({v[7] / nb:.0f} elems, tie rounds {v[10] / nb:.
       f"({v[6] / nb:.0f} elems)")
 print(f"  wave-busy per block: sorts {v[12] / nb / 100:.1f} us, partitions {v[13] / nb / 100:.1f} us "
       f"(/16 = {(v[12] + v[13]) / nb / 1600:.1f} us of the sort phase)")
+print("rc", L.bz2mi_debug_phases(5, buf))
+r = list(buf)
+nr = max(1, r[8])
+print(f"  deferred: {r[8]} blocks with deferred groups, {r[2] / nr:.0f} groups per such block (max {r[9]})")
 print("timings", ctx.timings())
