@@ -2371,17 +2371,17 @@ __global__ __launch_bounds__(FT) void bwt_block_small_kernel(const uint8_t* __re
 // being sorted.  BWT bytes and origPtr are written as positions become final.
 // Long repeats: rotations still tied after kTextTieCap bytes (two-rotation
 // groups: kTextPairCap) are not sorted further in the sort phase.  Their SA
-// entries are flagged (kUnres) and the group goes to a deferred list.  A
-// deferred group of bucket ss is ordered just before ss's copy step, when
-// every bucket processed earlier is complete and its rotations' positions are
-// known (isa): its rotations are compared on their shared text from the
-// group's depth on until they differ or reach a byte c whose bucket is
-// complete, where the positions of rotations i + d in bucket c decide (the
-// order of a pair sharing d bytes is the order of its rotations i + d).  A
-// repeat of ordinary text reaches such a byte within a few bytes, however long
-// the repeat.  Blocks it cannot finish (periodic blocks: no such byte within
-// kDeferScan bytes; a group of more than 64 rotations; a full work queue or
-// pair list) get redo[b] = 2 and go through the general path
+// entries are flagged (kUnres) and the group goes to a deferred list.  After
+// the sort phase, before any copy step, every deferred group is ordered
+// (text_resolve_all): a pair (i, j) sharing d bytes has the order of (i + x,
+// j + x) for any x <= d, so it is decided at the first x where both rotations
+// already have their final positions (sorted rotations: isa), or it links to
+// the deferred pair (i + x, j + x) -- the next one of the same repeat; the
+// links of a repeat form a chain down to the pair that meets the repeat's end,
+// collapsed by pointer jumping.  So a repeat of any length costs a few steps
+// per pair.  Blocks it cannot finish (periodic blocks, a group of more than 64
+// rotations, a group that waits on itself -- a tandem repeat --, a full work
+// queue or pair list) get redo[b] = 2 and go through the general path
 // (bwt_block_kernel mode 1).
 constexpr int kTextDcap = 512;    // depth at which a partition gives up
 constexpr int kTextChain = 32;    // levels a partition goes down with one child before its segment is deferred
@@ -2397,7 +2397,6 @@ constexpr int kTQ = 512;          // work items per round
 constexpr int kCopyR = 4;         // rotations per lane and chunk of a copy step
 constexpr int kTW = 768;          // per-wave LDS words
 constexpr uint32_t kUnres = 0x80000000u;  // SA entry flag: a member of a deferred group (not yet ordered)
-constexpr uint32_t kDeferScan = 4096;     // bytes a deferred comparison scans before the block goes back
 // non-empty (first, second byte) pairs of a text-path block (~2,000 in a 90 KB
 // block of real text): counted in the per-wave scratch during the setup, and
 // the pair list (uint64 entries) lives in the block's group area, which holds
@@ -2420,8 +2419,7 @@ struct TextLds {
     uint32_t cstart[257];             // first-byte bucket starts
     uint32_t tmp[FW];
     uint32_t wlo[FW], whi[FW];        // a wave's range of pair entries (the deal)
-    uint32_t qn[2], fail, nflag, ndef;
-    uint32_t doff[257];               // deferred groups per bucket rank (offsets into the sorted list)
+    uint32_t qn[2], fail, nflag, ndef, nitems;
     uint8_t order[256];               // bytes by ascending bucket size
     uint8_t rank[256];                // position of a byte in that order
     uint8_t target[256];
@@ -2451,6 +2449,19 @@ __device__ __forceinline__ uint32_t pe_owner(uint64_t e) { return (uint32_t)(e >
 // store: it read stale spill words.)
 __device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) { return *p; }
 
+// the block goes back to the general path; PHASES builds count the reasons
+// (g_tbk_res[10 + why]: 0 group > 64, 1 periodic, 2 no progress, 3 pair list,
+// 4 work queue, 5 partition depth)
+#ifdef BZ2MI_PHASES
+#define TBK_FAIL(why)                                  \
+    do {                                               \
+        atomicOr(&L.fail, 1u);                         \
+        atomicAdd(&g_tbk_res[10 + (why)], 1ull);       \
+    } while (0)
+#else
+#define TBK_FAIL(why) atomicOr(&L.fail, 1u)
+#endif
+
 __device__ __forceinline__ uint64_t tq_item(uint32_t start, uint32_t len, uint32_t depth) {
     return ((uint64_t)(depth & 0xffffu) << 34) | ((uint64_t)len << 17) | (uint64_t)start;  // start, len < 2^17
 }
@@ -2467,7 +2478,7 @@ __device__ __forceinline__ void tq_push(TextLds& L, int nxt, bool want, uint32_t
     if (want) {
         const uint32_t pos = base + (uint32_t)__popcll(m & __lanemask_lt());
         if (pos < (uint32_t)kTQ) L.q[nxt][pos] = tq_item(start, len, depth);
-        else atomicOr(&L.fail, 1u);
+        else TBK_FAIL(4);
     }
 }
 
@@ -2545,7 +2556,7 @@ __device__ __forceinline__ uint32_t dg_depth(uint64_t e) { return (uint32_t)(e >
 // 64 rotations sends the block back
 __device__ __forceinline__ void dg_push(TextLds& L, uint64_t* dl, bool want, uint32_t start, uint32_t len,
                                         uint32_t depth) {
-    if (want && len > 64u) atomicOr(&L.fail, 1u);
+    if (want && len > 64u) TBK_FAIL(0);
     const uint64_t m = __ballot(want);
     if (m == 0) return;
     uint32_t base = 0;
@@ -2554,34 +2565,25 @@ __device__ __forceinline__ void dg_push(TextLds& L, uint64_t* dl, bool want, uin
     if (want) dl[base + (uint32_t)__popcll(m & __lanemask_lt())] = dg_make(start, len, depth);
 }
 
-// Order of rotations i0 != i1 that share their first d bytes, when every
-// bucket of rank < s is complete (isa: their positions): -1 if i0 comes first,
-// 1 if i1 does, 0 if no answer within kDeferScan bytes (periodic).
+// Order of rotations i0 != i1 of deferred group g that share their first d
+// bytes (long repeats), before any copy step.  isa holds the final position
+// of every rotation already placed (sorted, or resolved), kNoIsa for the
+// rotations of the pair buckets the copy steps fill, and kDefMark | group for
+// the members of deferred groups.  Walking x = 1, 2, ...: differing bytes
+// decide (x >= d); so do rotations i + x whose positions are both known
+// (rotations that share x bytes keep the order of their rotations i + x).
+// Rotations i + x that are the two members of another deferred pair h give a
+// link (*link = h, *x): the order is h's.  Returns -1 (i0 first), 1 (i1
+// first), 3 (link), 2 (wait: they reach a deferred group of more than two or
+// the group itself -- a later round may know more), 0 (equal rotations: a
+// periodic block).
+constexpr uint32_t kNoIsa = 0xffffffffu;
+constexpr uint32_t kDefMark = 0x80000000u;
 __device__ __forceinline__ int text_cmp_deferred(const uint8_t* Tl, int n, uint32_t i0, uint32_t i1, uint32_t d,
-                                                 uint32_t s, const uint8_t* rank, const uint32_t* isa) {
-    uint32_t p0 = (i0 + d) % (uint32_t)n, p1 = (i1 + d) % (uint32_t)n;
-    for (uint32_t k = 0; k < kDeferScan; k += 4) {
-        const uint32_t x0 = load4(Tl, n, p0), x1 = load4(Tl, n, p1);
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const uint32_t c0 = (x0 >> (24 - 8 * b)) & 255u, c1 = (x1 >> (24 - 8 * b)) & 255u;
-            if (c0 != c1) return c0 < c1 ? -1 : 1;
-            if (rank[c0] < s) {
-                uint32_t q0 = p0 + b, q1 = p1 + b;
-                if (q0 >= (uint32_t)n) q0 -= (uint32_t)n;
-                if (q1 >= (uint32_t)n) q1 -= (uint32_t)n;
-                return isa[q0] < isa[q1] ? -1 : 1;
-            }
-        }
-        p0 += 4;
-        p1 += 4;
-        if (p0 >= (uint32_t)n) p0 -= (uint32_t)n;
-        if (p1 >= (uint32_t)n) p1 -= (uint32_t)n;
-    }
-    return 0;
-}
+                                                 uint32_t g, const uint32_t* isa, const uint64_t* dl, uint32_t* link,
+                                                 uint32_t* xo);
 
-// Tied items of a wave sort (W[0, tt): index | slot << 17 | group head << 26,
+// Tied items of a wave sort (W[0, tt): index | slot << 17 | group head << 26,// Tied items of a wave sort (W[0, tt): index | slot << 17 | group head << 26,
 // groups in slot order) at depth D: every group of exactly two rotations is
 // ordered by comparing the LDS text directly, 8 bytes at a time, up to
 // kTextPairCap bytes (one lane per pair; the repeats of text tie in pairs),
@@ -2677,18 +2679,12 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
 #ifndef TBK_PART_INL
 #define TBK_PART_INL __forceinline__
 #endif
-__device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out, uint32_t* orig,
-                          uint32_t* W, TextLds& L, uint64_t* dl) {
-    constexpr int E = kSmall / 64;
+__device__ TBK_SORT_INL void text_sort_pre(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out,
+                                            uint32_t* orig, uint32_t* W, TextLds& L, uint64_t* dl,
+                                            const uint32_t (&pre)[kSmall / 64]) {
     const int lane = lane_id();
     TBK_ASSERT(seg.start + seg.len <= (uint32_t)n && seg.len >= 2u && seg.len <= (uint32_t)kSmall, "sort seg", seg.start,
                seg.len);
-    uint32_t pre[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t g = (uint32_t)(e * 64 + lane);
-        pre[e] = g < seg.len ? ld_fresh(sa + seg.start + g) : 0u;
-    }
     Scratch s{};
     s.sa = sa;
     uint32_t tt;
@@ -2729,6 +2725,19 @@ __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, S
     }
 }
 
+__device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out,
+                                        uint32_t* orig, uint32_t* W, TextLds& L, uint64_t* dl) {
+    constexpr int E = kSmall / 64;
+    const int lane = lane_id();
+    uint32_t pre[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t g = (uint32_t)(e * 64 + lane);
+        pre[e] = g < seg.len ? ld_fresh(sa + seg.start + g) : 0u;
+    }
+    text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
+}
+
 // partition a segment of > kSmall rotations with a common prefix of d bytes
 // by byte d (one wave): children of one rotation are final, runs of small
 // ones go to the queue as batches, large ones as items of depth d+1.  A
@@ -2746,7 +2755,7 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     const uint32_t dcap = min((uint32_t)kTextDcap, d + (uint32_t)kTextChain);
     for (;;) {
         if (d >= dcap) {  // more than kSmall rotations sharing d bytes: the general path
-            if (lane == 0) atomicOr(&L.fail, 1u);
+            if (lane == 0) TBK_FAIL(5);
             return;
         }
         TBK_COUNT(5, 1);
@@ -2841,60 +2850,359 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     __builtin_amdgcn_wave_barrier();
 }
 
-// The deferred groups of bucket rank s (sorted list dl2[doff[s], doff[s+1])),
-// ordered with text_cmp_deferred: groups of two one per thread, larger ones
-// (up to 64) one per wave, every member ranked by comparing it with the
-// others.  Final SA entries, BWT bytes, origPtr and isa.
-__device__ void text_resolve_rank(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa, const uint64_t* dl2,
-                                  uint32_t s, uint8_t* out, uint32_t* orig, TextLds& L) {
-    const int t = threadIdx.x, w = wave_id(), lane = lane_id();
-    const uint32_t g0 = L.doff[s], g1 = L.doff[s + 1];
-    for (uint32_t g = g0 + (uint32_t)t; g < g1; g += FT) {
-        const uint64_t e = dl2[g];
-        if (dg_len(e) != 2) continue;
-        const uint32_t st = dg_start(e);
-        const uint32_t i0 = ld_fresh(sa + st) & 0x1ffffu, i1 = ld_fresh(sa + st + 1) & 0x1ffffu;
-        const int c = text_cmp_deferred(Tl, n, i0, i1, dg_depth(e), s, L.rank, isa);
-        if (c == 0) {
-            atomicOr(&L.fail, 1u);
-            continue;
+__device__ __forceinline__ int text_cmp_deferred(const uint8_t* Tl, int n, uint32_t i0, uint32_t i1, uint32_t d,
+                                                 uint32_t g, const uint32_t* isa, const uint64_t* dl, uint32_t* link,
+                                                 uint32_t* xo) {
+    uint32_t p0 = i0 + 1 < (uint32_t)n ? i0 + 1 : 0u, p1 = i1 + 1 < (uint32_t)n ? i1 + 1 : 0u;
+    for (uint32_t x = 1; x < (uint32_t)n; ++x) {
+        if (x >= d) {
+            const uint32_t c0 = Tl[p0], c1 = Tl[p1];
+            if (c0 != c1) return c0 < c1 ? -1 : 1;
         }
-        const uint32_t a = c < 0 ? i0 : i1, b = c < 0 ? i1 : i0;
-        sa[st] = a;
-        sa[st + 1] = b;
-        isa[a] = st;
-        isa[b] = st + 1;
-        text_final(Tl, n, st, a, out, orig);
-        text_final(Tl, n, st + 1, b, out, orig);
+        const uint32_t a0 = isa[p0], a1 = isa[p1];
+        if (a0 < kDefMark && a1 < kDefMark) return a0 < a1 ? -1 : 1;
+        if (a0 == a1 && a0 != kNoIsa) {  // both in deferred group h
+            const uint32_t h = a0 & ~kDefMark;
+            if (h == g) return 2;
+            *link = h;
+            *xo = x;
+            return 3;
+        }
+        if (++p0 == (uint32_t)n) p0 = 0;
+        if (++p1 == (uint32_t)n) p1 = 0;
     }
-    for (uint32_t gb = g0 + (uint32_t)w * 64; gb < g1; gb += FT) {
-        const uint32_t g = gb + (uint32_t)lane;
-        const uint64_t e = g < g1 ? dl2[g] : 0ull;
-        for (uint64_t mm = __ballot(g < g1 && dg_len(e) > 2); mm; mm &= mm - 1) {
-            const int l = __builtin_ctzll(mm);
-            const uint32_t lo = uniform((uint32_t)__shfl((int)(uint32_t)e, l));
-            const uint32_t hi = uniform((uint32_t)__shfl((int)(uint32_t)(e >> 32), l));
-            const uint64_t ee = ((uint64_t)hi << 32) | lo;
-            const uint32_t st = dg_start(ee), m = dg_len(ee), dep = dg_depth(ee);
-            const uint32_t me = (uint32_t)lane < m ? ld_fresh(sa + st + lane) & 0x1ffffu : 0u;
-            uint32_t below = 0;
-            bool bad = false;
-            for (uint32_t k = 0; k < m; ++k) {
-                const uint32_t other = (uint32_t)__shfl((int)me, (int)k);
-                if ((uint32_t)lane < m && k != (uint32_t)lane) {
-                    const int c = text_cmp_deferred(Tl, n, other, me, dep, s, L.rank, isa);
-                    below += c < 0 ? 1u : 0u;
-                    bad |= c == 0;
+    return 0;
+}
+
+constexpr uint64_t kDgDone = 1ull << 63;
+constexpr uint64_t kLkLink = 1ull << 62;  // link state of a pair: target << 32 | offset
+
+// a deferred pair's rotations in order: SA entries, isa, BWT bytes, origPtr
+__device__ __forceinline__ void dg_place(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa, uint8_t* out,
+                                         uint32_t* orig, uint32_t st, uint32_t a, uint32_t b) {
+    sa[st] = a;
+    sa[st + 1] = b;
+    isa[a] = st;
+    isa[b] = st + 1;
+    text_final(Tl, n, st, a, out, orig);
+    text_final(Tl, n, st + 1, b, out, orig);
+}
+
+// Order of rotations a != b from their first byte on, by bytes and known
+// positions only (deferred and not yet copied rotations are walked over):
+// -1 (a first), 1, or 0 (equal: periodic)
+__device__ __forceinline__ int text_cmp_plain(const uint8_t* Tl, int n, uint32_t a, uint32_t b, const uint32_t* isa) {
+    uint32_t p0 = a, p1 = b;
+    for (uint32_t x = 0; x < (uint32_t)n; ++x) {
+        const uint32_t c0 = Tl[p0], c1 = Tl[p1];
+        if (c0 != c1) return c0 < c1 ? -1 : 1;
+        const uint32_t a0 = isa[p0], a1 = isa[p1];
+        if (a0 < kDefMark && a1 < kDefMark) return a0 < a1 ? -1 : 1;
+        if (++p0 == (uint32_t)n) p0 = 0;
+        if (++p1 == (uint32_t)n) p1 = 0;
+    }
+    return 0;
+}
+
+// Rank of member k of deferred group g whose members' rotations i + x all
+// have known positions (isa): the members keep the order of their images.
+// Serial over the m members (m <= 64; nearly always 2 or 3).
+__device__ __forceinline__ void dg_place_by_images(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa,
+                                                   uint8_t* out, uint32_t* orig, uint32_t st, uint32_t m,
+                                                   uint32_t x) {
+    uint32_t mem[64], key[64];
+    for (uint32_t k = 0; k < m; ++k) {
+        mem[k] = ld_fresh(sa + st + k) & 0x1ffffu;
+        key[k] = isa[(mem[k] + x) % (uint32_t)n];
+    }
+    for (uint32_t k = 0; k < m; ++k) {
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < m; ++j) r += key[j] < key[k] ? 1u : 0u;
+        sa[st + r] = mem[k];
+        isa[mem[k]] = st + r;
+        text_final(Tl, n, st + r, mem[k], out, orig);
+    }
+}
+
+// Every deferred group of the block (dl[0, ndef)), ordered before the copy
+// steps.  Rounds of: (1) every open group walks x = 1, 2, ... (pairs: one
+// thread each, text_cmp_deferred; larger groups: one wave, a lane per
+// member) until its members' rotations i + x all have known positions --
+// placed by their order -- or all lie in one other deferred group h -- a link
+// (h, x): the group's order is that of its images in h; (2) pointer jumping
+// over the links (a group whose target is placed is placed by its images; one
+// whose target is linked takes that link, offsets added), so the chain of a
+// repeat -- group (i, j, ...) links to (i + x, j + x, ...), and so on down to
+// the group that meets the repeat's end -- collapses in a logarithmic number
+// of steps; (3) larger groups whose members' bytes part before any decision
+// rank every member by comparing it with the others.  A round that places
+// nothing sends the block back (a group waiting on itself: a tandem repeat).
+// lk: a state per group (0 open, kDgDone, or a link).
+__device__ void text_resolve_all(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa, const uint64_t* dl,
+                                 uint32_t ndef, uint64_t* lk, uint8_t* out, uint32_t* orig, TextLds& L) {
+    const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+    uint32_t* W = L.w[w];
+    for (uint32_t g = t; g < ndef; g += FT) lk[g] = 0;
+    __threadfence_block();
+    __syncthreads();
+    uint32_t before = 0xffffffffu;
+    bool forced = false;  // the previous round ordered the open roots by plain comparison
+    for (;;) {
+#ifdef BZ2MI_PHASES
+        if (t == 0) atomicAdd(&g_tbk_res[3], 1ull);
+#endif
+        // (1) pairs
+        for (uint32_t g = t; g < ndef; g += FT) {
+            const uint64_t e = dl[g];
+            if (dg_len(e) != 2 || lk[g] != 0) continue;
+            const uint32_t st = dg_start(e);
+            const uint32_t i0 = ld_fresh(sa + st) & 0x1ffffu, i1 = ld_fresh(sa + st + 1) & 0x1ffffu;
+            uint32_t h = 0, x = 0;
+            const int c = text_cmp_deferred(Tl, n, i0, i1, dg_depth(e), g, isa, dl, &h, &x);
+            if (c == 0) {
+                TBK_FAIL(1);
+                continue;
+            }
+            if (c == 2) continue;
+            if (c == 3) {
+                lk[g] = kLkLink | ((uint64_t)h << 32) | x;
+                continue;
+            }
+            dg_place(Tl, n, sa, isa, out, orig, st, c < 0 ? i0 : i1, c < 0 ? i1 : i0);
+            lk[g] = kDgDone;
+        }
+        // (1) larger groups: a wave each, lane = member, while the members
+        // share their bytes (x < depth)
+        for (uint32_t gb = (uint32_t)w * 64; gb < ndef; gb += FT) {
+            const uint32_t g = gb + (uint32_t)lane;
+            const uint64_t e = g < ndef ? dl[g] : 0ull;
+            for (uint64_t mm = __ballot(g < ndef && dg_len(e) > 2 && lk[g] == 0); mm; mm &= mm - 1) {
+                const int l = __builtin_ctzll(mm);
+                const uint32_t gg = gb + (uint32_t)l;
+                const uint32_t lo = uniform((uint32_t)__shfl((int)(uint32_t)e, l));
+                const uint32_t hi = uniform((uint32_t)__shfl((int)(uint32_t)(e >> 32), l));
+                const uint64_t ee = ((uint64_t)hi << 32) | lo;
+                const uint32_t st = dg_start(ee), m = dg_len(ee), dep = dg_depth(ee);
+                const bool mine = (uint32_t)lane < m;
+                const uint32_t me = mine ? ld_fresh(sa + st + lane) & 0x1ffffu : 0u;
+                for (uint32_t x = 1; x < dep; ++x) {
+                    const uint32_t a = mine ? isa[(me + x) % (uint32_t)n] : 0u;
+                    if (!__ballot(mine && a >= kDefMark)) {  // every image placed
+                        const uint32_t key = mine ? a : 0xffffffffu;
+                        uint32_t r = 0;
+                        for (uint32_t k = 0; k < m; ++k) r += (uint32_t)__shfl((int)key, (int)k) < key ? 1u : 0u;
+                        if (mine) {
+                            sa[st + r] = me;
+                            isa[me] = st + r;
+                            text_final(Tl, n, st + r, me, out, orig);
+                        }
+                        if (lane == 0) lk[gg] = kDgDone;
+                        break;
+                    }
+                    const uint32_t a0 = (uint32_t)__shfl((int)a, 0);
+                    if (a0 != kNoIsa && a0 >= kDefMark && (a0 & ~kDefMark) != gg && !__ballot(mine && a != a0)) {
+                        if (lane == 0) lk[gg] = kLkLink | ((uint64_t)(a0 & ~kDefMark) << 32) | x;
+                        break;
+                    }
                 }
             }
-            if (__ballot(bad) && lane == 0) atomicOr(&L.fail, 1u);
-            __builtin_amdgcn_wave_barrier();  // every lane has read its member before the writes
-            if ((uint32_t)lane < m) {
-                sa[st + below] = me;
-                isa[me] = st + below;
-                text_final(Tl, n, st + below, me, out, orig);
+        }
+        __threadfence_block();
+        __syncthreads();
+        // (2) links
+        for (int jump = 0; jump < 32; ++jump) {
+#ifdef BZ2MI_PHASES
+            if (t == 0) atomicAdd(&g_tbk_res[4], 1ull);
+#endif
+            if (t == 0) L.qn[1] = 0;
+            __syncthreads();
+            for (uint32_t g = t; g < ndef; g += FT) {
+                const uint64_t v = lk[g];
+                if (!(v & kLkLink)) continue;
+                const uint32_t h = (uint32_t)(v >> 32) & 0x3fffffffu, x = (uint32_t)v;
+                const uint64_t e = dl[g];
+                const uint32_t st = dg_start(e), m = dg_len(e);
+                bool known = true;
+                for (uint32_t k = 0; k < m && known; ++k)
+                    known = isa[((ld_fresh(sa + st + k) & 0x1ffffu) + x) % (uint32_t)n] < kDefMark;
+                if (known) {
+                    dg_place_by_images(Tl, n, sa, isa, out, orig, st, m, x);
+                    lk[g] = kDgDone;
+                    atomicAdd(&L.qn[1], 1u);
+                    continue;
+                }
+                const uint64_t th = lk[h];
+                if ((th & kLkLink) && (uint32_t)(th >> 32 & 0x3fffffffu) != g) {
+                    const uint32_t nx = x + (uint32_t)th;
+                    if (nx >= (uint32_t)n) {
+                        TBK_FAIL(1);
+                        continue;
+                    }
+                    lk[g] = kLkLink | (th & (0x3fffffffull << 32)) | nx;
+                    atomicAdd(&L.qn[1], 1u);
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            if (uniform(L.qn[1]) == 0 || uniform(L.fail)) break;  // nothing placed or jumped
+        }
+        // (3) larger groups still open: every member against the others
+        for (uint32_t gb = (uint32_t)w * 64; gb < ndef; gb += FT) {
+            const uint32_t g = gb + (uint32_t)lane;
+            const uint64_t e = g < ndef ? dl[g] : 0ull;
+            for (uint64_t mm = __ballot(g < ndef && dg_len(e) > 2 && lk[g] == 0); mm; mm &= mm - 1) {
+                const int l = __builtin_ctzll(mm);
+                const uint32_t lo = uniform((uint32_t)__shfl((int)(uint32_t)e, l));
+                const uint32_t hi = uniform((uint32_t)__shfl((int)(uint32_t)(e >> 32), l));
+                const uint64_t ee = ((uint64_t)hi << 32) | lo;
+                const uint32_t st = dg_start(ee), m = dg_len(ee), dep = dg_depth(ee);
+                const uint32_t me = (uint32_t)lane < m ? ld_fresh(sa + st + lane) & 0x1ffffu : 0u;
+                // a tandem repeat u^m t: the members (by position) step by the
+                // period P and the text is P-periodic from the first to the
+                // last; then their order is monotone -- every comparison
+                // reduces to u t against t, i.e. the last member against the
+                // rotation one period after it
+                {
+                    const uint32_t key = (uint32_t)lane < m ? me : 0xffffffffu;
+                    uint32_t pr = 0;  // rank by position
+                    for (uint32_t k = 0; k < m; ++k) pr += (uint32_t)__shfl((int)key, (int)k) < key ? 1u : 0u;
+                    if ((uint32_t)lane < m) W[pr] = me;
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t q0 = uniform(W[0]), P = uniform(W[1] - W[0]), qe = uniform(W[m - 1]);
+                    bool prog = true;
+                    for (uint32_t k = lane + 1; k < m; k += 64) prog &= W[k] - W[k - 1] == P;
+                    prog = !__ballot(!prog) && P > 0 && qe + P < (uint32_t)n;
+                    if (prog) {  // periodic over [q0, qe)?
+                        bool per = true;
+                        for (uint32_t x = q0 + lane; x < qe && per; x += 64) per = Tl[x] == Tl[x + P];
+                        prog = !__ballot(!per);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    if (prog) {
+                        int dir = 0;
+                        if (lane == 0) dir = text_cmp_plain(Tl, n, qe, qe + P, isa);
+                        dir = (int)uniform((uint32_t)dir);
+                        if (dir == 0) {
+                            if (lane == 0) TBK_FAIL(1);
+                            continue;
+                        }
+                        if ((uint32_t)lane < m) {
+                            const uint32_t slot = dir < 0 ? pr : m - 1 - pr;
+                            sa[st + slot] = me;
+                            isa[me] = st + slot;
+                            text_final(Tl, n, st + slot, me, out, orig);
+                        }
+                        if (lane == 0) lk[gb + l] = kDgDone;
+                        continue;
+                    }
+                }
+                uint32_t below = 0;
+                bool bad = false, wait = false;
+                for (uint32_t k = 0; k < m; ++k) {
+                    const uint32_t other = (uint32_t)__shfl((int)me, (int)k);
+                    if ((uint32_t)lane < m && k != (uint32_t)lane && !wait && !bad) {
+                        uint32_t h = 0, x = 0;
+                        const int c = text_cmp_deferred(Tl, n, other, me, dep, gb + l, isa, dl, &h, &x);
+                        below += c == -1 ? 1u : 0u;
+                        bad |= c == 0;
+                        wait |= c == 2 || c == 3;
+                    }
+                }
+                if (__ballot(bad)) {
+                    if (lane == 0) TBK_FAIL(1);
+                    continue;
+                }
+                if (__ballot(wait)) continue;
+                __builtin_amdgcn_wave_barrier();  // every lane has read its member before the writes
+                if ((uint32_t)lane < m) {
+                    sa[st + below] = me;
+                    isa[me] = st + below;
+                    text_final(Tl, n, st + below, me, out, orig);
+                }
+                if (lane == 0) lk[gb + l] = kDgDone;
             }
         }
+        __threadfence_block();
+        if (t == 0) L.qn[0] = 0;
+        __syncthreads();
+        for (uint32_t g = t; g < ndef; g += FT)
+            if (lk[g] != kDgDone) atomicAdd(&L.qn[0], 1u);
+        __syncthreads();
+        const uint32_t left = uniform(L.qn[0]);
+        if (left == 0 || uniform(L.fail)) break;
+        if (left >= before && !forced) {
+            // no group placed this round: the open groups that are not
+            // linked (the roots the linked ones wait on) are ordered by plain
+            // comparison -- bytes and known positions only, walking over the
+            // rest (however long) -- and the rounds go on
+            for (uint32_t gb = (uint32_t)w * 64; gb < ndef; gb += FT) {
+                const uint32_t g = gb + (uint32_t)lane;
+                const bool root = g < ndef && lk[g] == 0;
+                for (uint64_t mm = __ballot(root); mm; mm &= mm - 1) {
+                    const int l = __builtin_ctzll(mm);
+                    const uint64_t ee = dl[gb + l];
+                    const uint32_t st = dg_start(ee), m = dg_len(ee);
+                    const uint32_t me = (uint32_t)lane < m ? ld_fresh(sa + st + lane) & 0x1ffffu : 0u;
+                    uint32_t below = 0;
+                    bool bad = false;
+                    for (uint32_t k = 0; k < m; ++k) {
+                        const uint32_t other = (uint32_t)__shfl((int)me, (int)k);
+                        if ((uint32_t)lane < m && k != (uint32_t)lane && !bad) {
+                            const int c = text_cmp_plain(Tl, n, other, me, isa);
+                            below += c == -1 ? 1u : 0u;
+                            bad |= c == 0;
+                        }
+                    }
+                    if (__ballot(bad)) {
+                        if (lane == 0) TBK_FAIL(1);
+                        continue;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    if ((uint32_t)lane < m) {
+                        sa[st + below] = me;
+                        isa[me] = st + below;
+                        text_final(Tl, n, st + below, me, out, orig);
+                    }
+                    if (lane == 0) lk[gb + l] = kDgDone;
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            forced = true;
+#ifdef BZ2MI_PHASES
+            if (t == 0) atomicAdd(&g_tbk_res[7], 1ull);
+#endif
+            continue;
+        }
+        forced = false;
+        if (left >= before) {  // no group placed this round, nor by the plain comparisons
+            if (t == 0) TBK_FAIL(2);
+#ifdef TBK_NOPROG_DEBUG
+            if (t == 0) {
+                int shown = 0;
+                for (uint32_t g = 0; g < ndef && shown < 4; ++g) {
+                    if (lk[g] == kDgDone) continue;
+                    const uint64_t e = dl[g];
+                    const uint32_t st = dg_start(e), m = dg_len(e);
+                    printf("[noprog] block %d n %d group %u/%u len %u depth %u lk %llx members", (int)blockIdx.x, n, g,
+                           ndef, m, dg_depth(e), (unsigned long long)lk[g]);
+                    for (uint32_t k = 0; k < m && k < 6; ++k) printf(" %u", ld_fresh(sa + st + k) & 0x1ffffu);
+                    printf("\n");
+                    for (uint32_t x = 1; x < 6; ++x) {
+                        printf("   x=%u:", x);
+                        for (uint32_t k = 0; k < m && k < 6; ++k) {
+                            const uint32_t i = ld_fresh(sa + st + k) & 0x1ffffu;
+                            printf(" %08x", isa[(i + x) % (uint32_t)n]);
+                        }
+                        printf("\n");
+                    }
+                    ++shown;
+                }
+            }
+#endif
+            break;
+        }
+        before = left;
     }
 }
 
@@ -2969,6 +3277,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         if ((q0 & 7u) == 0) L.rowoff[q0 >> 3] = ex;
     }
     if (P > min((uint32_t)kPairCap, (uint32_t)bwt_group_stride(stride))) {  // uniform (a workgroup sum)
+#ifdef BZ2MI_PHASES
+        if (t == 0) atomicAdd(&g_tbk_res[13], 1ull);
+#endif
         if (t == 0) redo[b] = 2u;
         return;
     }
@@ -3048,30 +3359,63 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     tk1 = wall_clock64();
 #endif
     if (t < 2) L.qn[t] = 0;
-    {
-        const uint32_t per = (P + FT - 1) / FT;
-        const uint32_t e0 = (uint32_t)t * per, e1 = min(P, e0 + per);
-        uint32_t sum = 0;
-        for (uint32_t e = e0; e < e1; ++e) {
-            const uint64_t v = pl[e];
-            const uint32_t len = pe_len(v);
-            if (pe_expl(v) && len >= 2) sum += text_work(len);
+    if (t == 0) L.nitems = 0;
+    __syncthreads();
+    // sort items (dl2, free until the deferred groups are sorted): a thread
+    // per first-byte row walks its pair buckets in order; runs of consecutive
+    // explicit pairs of <= kSmall / 2 rotations become batches of <= kSmall
+    // (sorted from depth 1: the second byte separates them), larger pairs
+    // items of their own (depth 2: a wave sort or a partition); explicit
+    // pairs of one rotation are final.  (cnt[j] is pair j's end after the
+    // scatter, so its start is cnt[j - 1].)
+    if (t < 256) {
+        const uint32_t a = (uint32_t)t, ra = L.rank[a];
+        uint32_t j = rowpre[a * 8];
+        uint32_t bst = 0, blen = 0, bcnt = 0;
+        auto flush = [&]() {
+            if (blen >= 2) dl2[atomicAdd(&L.nitems, 1u)] = tq_item(bst, blen, bcnt > 1 ? 1u : 2u);
+            else if (blen == 1) text_final(Tl, n, bst, ld_fresh(sa + bst), out, orig);
+            blen = bcnt = 0;
+        };
+        for (uint32_t wq = 0; wq < 8; ++wq) {
+            uint32_t m = L.mask[a][wq];
+            while (m) {
+                const uint32_t c2 = wq * 32 + (uint32_t)__builtin_ctz(m);
+                m &= m - 1;
+                const uint32_t st = j ? cnt[j - 1] : 0u, len = cnt[j] - st;
+                ++j;
+                if (!(L.rank[c2] >= ra || ra < s_big)) {
+                    flush();
+                    continue;
+                }
+                if (len > (uint32_t)kSmall / 2) {
+                    flush();
+                    dl2[atomicAdd(&L.nitems, 1u)] = tq_item(st, len, 2u);
+                    continue;
+                }
+                if (blen + len > (uint32_t)kSmall) flush();
+                if (blen == 0) bst = st;
+                blen += len;
+                bcnt++;
+            }
         }
+        flush();
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t nitems = uniform(L.nitems);
+    {
+        // deal the items in equal shares of work (contiguous ranges of the list)
+        const uint32_t per = (nitems + FT - 1) / FT;
+        const uint32_t e0 = min(nitems, (uint32_t)t * per), e1 = min(nitems, e0 + per);
+        uint32_t sum = 0;
+        for (uint32_t e = e0; e < e1; ++e) sum += text_work((uint32_t)(dl2[e] >> 17) & 0x1ffffu);
         uint32_t total;
         uint32_t run = wg_excl_sum<FT>(sum, L.tmp, &total);
         for (uint32_t e = e0; e < e1; ++e) {
-            const uint64_t v = pl[e];
-            const uint32_t len = pe_len(v);
-            if (!pe_expl(v)) continue;
-            if (len == 1) {
-                const uint32_t st = pe_start(v);
-                text_final(Tl, n, st, ld_fresh(sa + st), out, orig);
-                continue;
-            }
-            const uint32_t wk = text_work(len);
+            const uint32_t wk = text_work((uint32_t)(dl2[e] >> 17) & 0x1ffffu);
             const uint32_t o = text_owner(run, wk, total);
             run += wk;
-            pl[e] = v | ((uint64_t)o << 51);
             atomicMin(&L.wlo[o], e);
             atomicMax(&L.whi[o], e + 1);
         }
@@ -3079,28 +3423,40 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     __threadfence_block();
     __syncthreads();
     {
+        // this wave's items, the next one's SA entries loaded while the
+        // current one is sorted
         const uint32_t lo = uniform(L.wlo[w]), hi = uniform(L.whi[w]);
-        for (uint32_t e0 = lo; e0 < hi; e0 += 64) {
-            const uint32_t e = e0 + (uint32_t)lane;
-            const uint64_t v = e < hi ? pl[e] : 0ull;
-            const bool mine = e < hi && pe_expl(v) && pe_len(v) >= 2 && pe_owner(v) == (uint32_t)w;
-            for (uint64_t m = __ballot(mine); m; m &= m - 1) {
-                if (uniform(*(volatile uint32_t*)&L.fail)) break;  // the block goes back to the general path
-                const int l = __builtin_ctzll(m);
-                const uint32_t vs = (uint32_t)__shfl((int)(uint32_t)v, l);
-                const uint32_t vl = (uint32_t)__shfl((int)(uint32_t)(v >> 17), l);
-                const Seg seg{uniform(vs & 0x1ffffu), uniform(vl & 0x1ffffu)};
-                TBK_T(2, seg.len);
-#ifdef BZ2MI_PHASES
-                const unsigned long long ti0 = wall_clock64();
-#endif
-                if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, 2, out, orig, W, L, dl);
-                else text_partition(Tl, n, sa, spill, seg, 2, out, orig, W, L, 0);
-                TBK_T(10, seg.len);
-#ifdef BZ2MI_PHASES
-                TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
-#endif
+        constexpr int E = kSmall / 64;
+        uint32_t pre[E];
+        auto load = [&](uint32_t k, uint32_t (&dst)[E]) {
+            const uint64_t it = dl2[k];
+            const uint32_t st = (uint32_t)it & 0x1ffffu, len = (uint32_t)(it >> 17) & 0x1ffffu;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint32_t g = (uint32_t)(e * 64 + lane);
+                dst[e] = (len <= (uint32_t)kSmall && g < len) ? ld_fresh(sa + st + g) : 0u;
             }
+        };
+        if (lo < hi) load(lo, pre);
+        for (uint32_t k = lo; k < hi; ++k) {
+            if (uniform(*(volatile uint32_t*)&L.fail)) break;  // the block goes back to the general path
+            uint32_t nxt[E];
+            if (k + 1 < hi) load(k + 1, nxt);
+            const uint64_t it = dl2[k];
+            const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
+            const uint32_t d = uniform((uint32_t)(it >> 34) & 0xffffu);
+            TBK_T(2, seg.len);
+#ifdef BZ2MI_PHASES
+            const unsigned long long ti0 = wall_clock64();
+#endif
+            if (seg.len <= (uint32_t)kSmall) text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
+            else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, 0);
+            TBK_T(10, seg.len);
+#ifdef BZ2MI_PHASES
+            TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
+#endif
+#pragma unroll
+            for (int e = 0; e < E; ++e) pre[e] = nxt[e];
         }
     }
     __threadfence_block();
@@ -3160,47 +3516,34 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
     tks = wall_clock64() - tk1;
 #endif
-    // ---- deferred groups: isa (the position of every final rotation so far,
-    // in spill: free after the sort phase), the groups sorted by the rank of
-    // their bucket, then the groups of the buckets sorted whole (ranks before
-    // s_big) ordered in ascending rank -- each sees every earlier bucket
-    // complete
+    // ---- deferred groups (long repeats), every one before the copy steps:
+    // isa (in spill, free after the sort phase) = the positions known now
+    // (every sorted rotation; kNoIsa for the pair buckets (x, c) the copy
+    // steps fill -- rank(x) >= s_big, rank(c) < rank(x) -- and kDefMark | g for
+    // the members of deferred group g)
     const uint32_t ndef = uniform(L.ndef);
-    const bool need_isa = ndef != 0 && !uniform(L.fail);
     uint32_t* isa = spill;
 #ifdef BZ2MI_PHASES
     unsigned long long tkr = wall_clock64();
 #endif
-    if (need_isa) {
+    if (ndef != 0 && !uniform(L.fail)) {
         for (uint32_t k = t; k < (uint32_t)n; k += FT) {
-            const uint32_t v = ld_fresh(sa + k);
-            if (!(v & kUnres)) isa[v] = k;
-        }
-        if (t < 257) L.doff[t] = 0;
-        __syncthreads();
-        for (uint32_t g = t; g < ndef; g += FT)
-            atomicAdd(&L.doff[L.rank[Tl[ld_fresh(sa + dg_start(dl[g])) & 0x1ffffu]]], 1u);
-        __syncthreads();
-        uint32_t tot;
-        const uint32_t ex = wg_excl_sum<FT>(t < 256 ? L.doff[t] : 0u, L.tmp, &tot);
-        if (t < 256) {
-            L.doff[t] = ex;
-            L.pcol[t] = ex;
-        }
-        if (t == 0) L.doff[256] = tot;
-        __syncthreads();
-        for (uint32_t g = t; g < ndef; g += FT) {
-            const uint64_t e = dl[g];
-            dl2[atomicAdd(&L.pcol[L.rank[Tl[ld_fresh(sa + dg_start(e)) & 0x1ffffu]]], 1u)] = e;
+            const uint32_t v = ld_fresh(sa + k), i = v & 0x1ffffu;
+            const uint32_t rx = L.rank[Tl[i]], rc = L.rank[Tl[i + 1 < (uint32_t)n ? i + 1 : 0u]];
+            const bool implicit = rx >= s_big && rc < rx;
+            isa[i] = (implicit || (v & kUnres)) ? kNoIsa : k;
         }
         __threadfence_block();
         __syncthreads();
-        for (uint32_t s = s0; s < s_big; ++s) {
-            if (L.doff[s + 1] == L.doff[s]) continue;  // (uniform: LDS after a barrier)
-            text_resolve_rank(Tl, n, sa, isa, dl2, s, out, orig, L);
-            __threadfence_block();
-            __syncthreads();
+        for (uint32_t g = t; g < ndef; g += FT) {
+            const uint64_t e = dl[g];
+            for (uint32_t k = 0; k < dg_len(e); ++k) isa[ld_fresh(sa + dg_start(e) + k) & 0x1ffffu] = kDefMark | g;
         }
+        __threadfence_block();
+        __syncthreads();
+        text_resolve_all(Tl, n, sa, isa, dl, ndef, dl2, out, orig, L);
+        __threadfence_block();
+        __syncthreads();
     }
 #ifdef BZ2MI_PHASES
     tkr = wall_clock64() - tkr;
@@ -3244,7 +3587,6 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                 if (tgt) {
                     const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
                     sa[bs + below] = j;
-                    if (need_isa) isa[j] = bs + below;
                     text_final(Tl, n, bs + below, j, out, orig);
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -3264,18 +3606,6 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
         tk1 = wall_clock64();
 #endif
-        if (need_isa && L.doff[s + 1] > L.doff[s]) {  // bucket ss's deferred groups first
-#ifdef BZ2MI_PHASES
-            const unsigned long long tr0 = wall_clock64();
-#endif
-            text_resolve_rank(Tl, n, sa, isa, dl2, s, out, orig, L);
-            __threadfence_block();
-            __syncthreads();
-#ifdef BZ2MI_PHASES
-            tkr += wall_clock64() - tr0;
-#endif
-            if (uniform(L.fail)) break;
-        }
         bool tg = false;
         if (t < 256) {
             const uint32_t x = (uint32_t)t, wq = ss >> 5, bit = ss & 31u;
@@ -3342,7 +3672,6 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                         const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
                         const uint32_t pos = bs + below;
                         sa[pos] = jv[r];
-                        if (need_isa) isa[jv[r]] = pos;
                         text_final(Tl, n, pos, jv[r], out, orig);
                         if (below == 0) C[x] = bs + (uint32_t)__popcll(peers);
                     }

@@ -36,5 +36,9 @@ print(f"  wave-busy per block: sorts {v[12] / nb / 100:.1f} us, partitions {v[13
 print("rc", L.bz2mi_debug_phases(5, buf))
 r = list(buf)
 nr = max(1, r[8])
-print(f"  deferred: {r[8]} blocks with deferred groups, {r[2] / nr:.0f} groups per such block (max {r[9]})")
+print(f"  deferred: {r[8]} blocks with deferred groups, {r[2] / nr:.0f} groups per such block (max {r[9]}); "
+      f"sent back: group>64 {r[10]}, periodic {r[11]}, no progress {r[12]}, pair list {r[13]}, work queue {r[14]}, "
+      f"partition depth {r[15]}")
+print(f"  resolve work per deferring block: rounds {r[3] / nr:.1f}, jump iterations {r[4] / nr:.1f}, plain-comparison "
+      f"passes {r[7]} in all")
 print("timings", ctx.timings())
