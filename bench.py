@@ -55,7 +55,9 @@ def ensure_built():
         subprocess.run(["make", "-C", PKG, "-j8"], check=True, stdout=subprocess.DEVNULL)
 
 
-TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r03_traffic_{data}.json")
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r04_traffic_{data}.json")
+ISSUE_PROFILE = os.path.join(REPO, "profiles", "r04_issue_{data}.json")
+KSTATS_PROFILE = "profiles/r04_kernel_stats_{data}_v1.csv"
 # the kernels of each timed stage (bz2mi_compress_device, csrc/api.hip)
 STAGE_KERNELS = {
     "front": "fe_summary/runscan/costscan/dmap/chain/resolve (scans + block chain) and fe_rle1_kernel",
@@ -82,6 +84,33 @@ def stage_traffic(args, stage):
         return int(prof["stages"][stage]["traffic_bytes"]), os.path.relpath(path, REPO)
     except (OSError, KeyError, ValueError):
         return None, None
+
+
+ISSUE_PREFIX = {"front": ("fe_",), "bwt": ("bwt_",), "mtf": ("mtf_kernel",), "huffman": ("huffman_kernel",),
+                "assemble": ("assemble", "offsets_dev", "advance")}
+
+
+def stage_issue(args, stage):
+    """VALU issue utilisation and LDS bank-conflict share of the stage's
+    kernels, from the committed SQ/GRBM --pmc pass of this same command
+    (tools/r4_measure.sh -> tools/issue.py); kernels taking <2% of the stage's
+    profiled time are left out."""
+    if args.mib != 1024 or args.level != 9 or args.parallel != 10 or args.unit != 10000:
+        return None
+    path = ISSUE_PROFILE.format(data=args.data)
+    try:
+        with open(path) as f:
+            prof = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ks = {k: v for k, v in prof["kernels"].items() if k.startswith(ISSUE_PREFIX[stage])}
+    tot = sum(v["ms_total"] for v in ks.values()) or 1.0
+    keep = {k: {a: v[a] for a in ("valu_issue_frac", "lds_bank_conflict_frac", "salu_per_valu", "eff_clock_GHz")
+                if a in v} | {"time_share": round(v["ms_total"] / tot, 3)}
+            for k, v in ks.items() if v["ms_total"] >= 0.02 * tot}
+    return {"source": os.path.relpath(path, REPO), "kernels": keep,
+            "what": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE/8): the share of SIMD issue "
+                    "slots the kernel's VALU stream used; SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE"}
 
 
 def host_cpu() -> dict:
@@ -341,9 +370,10 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
             "algorithmic_bytes": int(alg[dom]), "avg_ms": round(avg[dom], 3),
             "stage_kernels": STAGE_KERNELS.get(dom),
+            "issue": stage_issue(args, dom),
             "what": "HIP events around the stage's launches on the stream they run on, per step; the stage is "
-                    "the kernels listed (their rocprofv3 durations sum to avg_ms: profiles/r03_kernel_stats_"
-                    + args.data + "_v2.csv)",
+                    "the kernels listed (their rocprofv3 durations sum to avg_ms: "
+                    + KSTATS_PROFILE.format(data=args.data) + ")",
             "pipeline_GBps": round((n + out_len) / (ms_step * 1e-3) / 1e9, 2),
             "stage_ms": {k: round(v, 3) for k, v in avg.items()}}
     # the metric's literal wording, "900KB blocks": the same input at -9 in the

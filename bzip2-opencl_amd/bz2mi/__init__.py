@@ -100,11 +100,14 @@ def lib() -> ctypes.CDLL:
                                     c.c_size_t, c.POINTER(c.c_uint64), c.POINTER(c.c_size_t), c.POINTER(c.c_int)]
     L.bz2mi_dlast_timings.restype = c.c_int
     L.bz2mi_dlast_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
-    L.bz2mi_dlast_trailing.restype = c.c_int
-    L.bz2mi_dlast_trailing.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
-    L.bz2mi_abi_version.restype = c.c_int
-    if L.bz2mi_abi_version() != ABI_VERSION:
-        raise RuntimeError(f"{LIB_PATH}: ABI {L.bz2mi_abi_version()}, this binding expects {ABI_VERSION}")
+    if hasattr(L, "bz2mi_abi_version"):
+        L.bz2mi_dlast_trailing.restype = c.c_int
+        L.bz2mi_dlast_trailing.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
+        L.bz2mi_abi_version.restype = c.c_int
+        if L.bz2mi_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH}: ABI {L.bz2mi_abi_version()}, this binding expects {ABI_VERSION}")
+    elif not os.environ.get("BZ2MI_LIBRARY"):  # (an older library loaded on purpose for an A/B run)
+        raise RuntimeError(f"{LIB_PATH}: no bz2mi_abi_version (a library older than ABI {ABI_VERSION})")
     L.bz2mi_unit_halo.restype = c.c_size_t
     L.bz2mi_unit_halo.argtypes = [c.c_int, c.c_int]
     L.bz2mi_unit_create.restype = c.c_void_p
