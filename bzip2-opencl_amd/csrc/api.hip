@@ -112,8 +112,13 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     if (nb > c->bwtq_blocks) {  // queues are shared by the batches: BWTs run one at a time
         HIPCHECK(hipStreamSynchronize(s));
         for (void* p : {(void*)c->d_sq, (void*)c->d_lq[0], (void*)c->d_lq[1], (void*)c->d_tq[0], (void*)c->d_tq[1],
-                        (void*)c->d_tc, (void*)c->d_lspill, (void*)c->d_scb})
+                        (void*)c->d_tc, (void*)c->d_lspill, (void*)c->d_scb, (void*)c->d_dscratch,
+                        (void*)c->d_dlist[0], (void*)c->d_dlist[1], (void*)c->d_dlarge[0], (void*)c->d_dlarge[1],
+                        (void*)c->d_dctr})
             if (p) (void)hipFree(p);
+        c->d_dscratch = nullptr;
+        c->d_dlist[0] = c->d_dlist[1] = c->d_dlarge[0] = c->d_dlarge[1] = nullptr;
+        c->d_dctr = nullptr;
         c->d_sq = nullptr;
         c->d_lq[0] = c->d_lq[1] = nullptr;
         c->d_tq[0] = c->d_tq[1] = nullptr;
@@ -132,6 +137,14 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         if ((r = dalloc(&c->d_tc, 2 * B))) return r;
         if ((r = dalloc(&c->d_lspill, B * c->stride))) return r;
         if ((r = dalloc(&c->d_scb, B))) return r;
+        if (c->S > kBwtLdsText) {
+            if ((r = dalloc(&c->d_dscratch, B * dbl_slot_bytes(c->S)))) return r;
+            for (int k = 0; k < 2; ++k) {
+                if ((r = dalloc(&c->d_dlist[k], B * dbl_list_cap(c->S)))) return r;
+                if ((r = dalloc(&c->d_dlarge[k], B * dbl_large_cap(c->S)))) return r;
+            }
+            if ((r = dalloc(&c->d_dctr, (size_t)kDblCtr * (kDblMaxRounds + 2)))) return r;
+        }
         c->bwtq_blocks = (int)B;
     }
     const size_t Bs = ((size_t)c->bwtq_blocks + kBwtShards - 1) / kBwtShards;
@@ -229,17 +242,59 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
                            t.d_sa, t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_tq[0], tc[0], tcap);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_small");
-    for (int r = 0; r < kBwtTieRounds; ++r) {
-        hipLaunchKernelGGL(bwt_tie_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, t.d_sa,
+    // tie rounds of 8 bytes, then the doubling (fewer on the grid path, whose
+    // doubling resolves long repeated passages directly)
+    // (big blocks: 8 workgroups per block, each a slice of its list)
+    const int tie_rounds = blk ? kBwtTieRounds : kBwtTieRoundsGrid;
+    const unsigned tie_split = blk ? 1u : 8u;
+    for (int r = 0; r < tie_rounds; ++r) {
+        HIPCHECK(hipMemsetAsync(tc[(r + 1) & 1], 0, nb * sizeof(uint32_t), s));
+        hipLaunchKernelGGL(bwt_tie_kernel, dim3(nb, tie_split), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, t.d_sa,
                            t.d_bwt, t.d_orig, c->d_tq[r & 1], tc[r & 1], c->d_tq[(r + 1) & 1], tc[(r + 1) & 1], tcap,
-                           t.d_groups, t.d_ngroups, t.d_p2list, p2count, r + 1 == kBwtTieRounds ? 1 : 0);
+                           t.d_groups, t.d_ngroups, t.d_p2list, p2count, r + 1 == tie_rounds ? 1 : 0);
         HIPCHECK(hipGetLastError());
     }
     STAGE_DONE("bwt_ties");
-    hipLaunchKernelGGL(bwt_double_kernel, dim3(slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
-                       t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, t.d_groups, t.d_ngroups,
-                       t.d_p2list, p2count, pull);
-    HIPCHECK(hipGetLastError());
+    if (blk) {
+        hipLaunchKernelGGL(bwt_double_kernel, dim3(slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
+                           t.d_sa, t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, t.d_groups,
+                           t.d_ngroups, t.d_p2list, p2count, pull);
+        HIPCHECK(hipGetLastError());
+    } else {
+        // grid-wide doubling: every launch returns at once when nothing is left
+        DblGrid G{t.d_blocks, c->stride, t.d_lens, t.d_sa, t.d_bwt, t.d_orig, t.d_groups, t.d_ngroups, t.d_p2list,
+                  p2count, c->d_dscratch, dbl_slot_bytes(c->S), c->S, {c->d_dlist[0], c->d_dlist[1]},
+                  {c->d_dlarge[0], c->d_dlarge[1]}, c->d_dctr};
+        const dim3 grid((unsigned)c->cus * 8), blk256(256);
+        HIPCHECK(hipMemsetAsync(c->d_dctr, 0, sizeof(uint32_t) * kDblCtr * (kDblMaxRounds + 2), s));
+        hipLaunchKernelGGL(dbl_init_rank_kernel, grid, blk256, 0, s, G);
+        hipLaunchKernelGGL(dbl_init_groups_kernel, grid, blk256, 0, s, G);
+        const int R = dbl_rounds(c->S);
+        for (int r = 0; r < R; ++r) {
+            hipLaunchKernelGGL(dbl_pairset_kernel, grid, blk256, 0, s, G, r);
+            hipLaunchKernelGGL(dbl_runend_kernel, grid, blk256, 0, s, G, r);
+            hipLaunchKernelGGL(dbl_decide_kernel, grid, blk256, 0, s, G, r);
+            hipLaunchKernelGGL(dbl_snap_kernel, grid, blk256, 0, s, G, r);
+            hipLaunchKernelGGL(dbl_sort_kernel, grid, blk256, 0, s, G, r);
+            hipLaunchKernelGGL(dbl_large_kernel, grid, blk256, 0, s, G, r);
+        }
+        hipLaunchKernelGGL(dbl_emit_kernel, grid, blk256, 0, s, G);
+        HIPCHECK(hipGetLastError());
+        if (getenv("BZ2MI_DBL_STATS")) {  // debug: per-round group counts
+            std::vector<uint32_t> h((size_t)kDblCtr * (kDblMaxRounds + 2));
+            uint32_t np = 0;
+            HIPCHECK(hipMemcpyAsync(h.data(), c->d_dctr, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipMemcpyAsync(&np, p2count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "[bz2mi] doubling: %u blocks\n", np);
+            for (int r = 0; r < R; ++r) {
+                const uint32_t* q = &h[(size_t)kDblCtr * r];
+                if (q[0] + q[2] == 0) break;
+                fprintf(stderr, "  round %d: groups %u large %u -> kept %u; pairs on %u decided %u undecided %u\n", r,
+                        q[0], q[2], q[1], q[6], q[3], q[4]);
+            }
+        }
+    }
     STAGE_DONE("bwt");
     return BZ2MI_OK;
 }
@@ -690,7 +745,7 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
             occ = 4;
         c->wlevel_grid = std::max(8, cus * occ / 8 * 8);
     }
-    if (dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S)) ||
+    if ((c->S <= bz2mi::kBwtLdsText && dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S))) ||
         dalloc(&c->d_lscratch, c->level_slots * bz2mi::bwt_level_slot_bytes(c->S)) ||
         dalloc(&c->d_state, (size_t)c->p * bz2mi::kMaxAlpha) || dalloc(&c->d_sd, 1) || dalloc(&c->d_vol, 4)) {
         bz2mi_destroy(c);
@@ -711,6 +766,10 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     // scatter); after it one batch and batches of 3072 both give 26.0 -- one
     // batch keeps the per-stage event times per launch (the roofline figures).
     c->batch_blocks = std::min(16384, std::max(64, (int)((1536u << 20) / (unsigned)c->S)));
+    if (c->S > bz2mi::kBwtLdsText) {  // the grid doubling's scratch: about 24 GB per batch at most
+        const size_t per = bz2mi::dbl_slot_bytes(c->S) + 16 * (bz2mi::dbl_list_cap(c->S) + bz2mi::dbl_large_cap(c->S));
+        c->batch_blocks = std::min(c->batch_blocks, std::max(64, (int)((size_t)24e9 / per)));
+    }
     if (const char* e = getenv("BZ2MI_BATCH_BLOCKS")) c->batch_blocks = std::max(1, atoi(e));
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     if (hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess) {
@@ -726,7 +785,8 @@ void bz2mi_destroy(bz2mi_ctx* c) {
     (void)hipSetDevice(c->device);
     for (hipStream_t st : {c->stream, c->sA, c->sM, c->sB, c->sF})
         if (st) (void)hipStreamSynchronize(st);
-    std::vector<void*> ptrs = {c->d_out, c->d_scratch, c->d_sq, c->d_lq[0], c->d_lq[1], c->d_tq[0], c->d_tq[1],
+    std::vector<void*> ptrs = {c->d_dscratch, c->d_dlist[0], c->d_dlist[1], c->d_dlarge[0], c->d_dlarge[1], c->d_dctr,
+                               c->d_out, c->d_scratch, c->d_sq, c->d_lq[0], c->d_lq[1], c->d_tq[0], c->d_tq[1],
                                c->d_tc, c->d_lscratch, c->d_lspill, c->d_scb, c->d_state, c->d_crctab, c->d_sd, c->d_vol, c->d_ostage, c->d_in,
                                c->d_hout};
     for (int k = 0; k < 2; ++k) {
@@ -924,6 +984,7 @@ int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
         case 3: return bz2mi::fe_phases(out16);
         case 4: return bz2mi::tbk_stats(out16);
         case 5: return bz2mi::tbk_resolve_stats(out16);
+        case 6: return bz2mi::dbl_stats(out16);
         default: return BZ2MI_EINVAL;
     }
 }

@@ -32,6 +32,7 @@ namespace bz2mi {
 BZ2MI_PHASE_TABLE(g_bwt_phase)
 BZ2MI_PHASE_TABLE(g_tbk_stat)
 BZ2MI_PHASE_TABLE(g_tbk_res)  // text_resolve sums (PHASES builds)
+BZ2MI_PHASE_TABLE(g_dbl_stat)  // bwt_finish sums (PHASES builds)
 #ifdef TBK_TRACE
 __device__ unsigned int* g_tbk_trace;
 #endif
@@ -59,6 +60,15 @@ int tbk_stats(unsigned long long* out) {
 int tbk_resolve_stats(unsigned long long* out) {
 #ifdef BZ2MI_PHASES
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbk_res), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
+    (void)out;
+    return 0;
+#endif
+}
+
+int dbl_stats(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbl_stat), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
 #else
     (void)out;
     return 0;
@@ -93,6 +103,7 @@ struct BwtShared {
     uint32_t bcast[4];
     uint32_t bat_start[256];  // batches of small children (pack_children)
     uint32_t bat_len[256];    // length | one-child flag << 31
+    uint32_t wfirst[NW];      // resolve_pairs: first run end in each wave's range
 };
 
 using Seg = BwtSeg;
@@ -529,8 +540,10 @@ __device__ void radix_pass(const uint64_t* kin, const uint32_t* vin, uint64_t* k
 }
 
 // Sort a large phase-2 group [start, start+len) by (snapshot key, index) with
-// the whole workgroup, then relabel and emit subgroups.
-__device__ void wg_sort_group(Scratch& s, Seg seg, BwtShared& sh, Seg* out, uint32_t* counter) {
+// the whole workgroup, then relabel and emit subgroups (emit(Seg), one thread
+// per subgroup).
+template <class Emit>
+__device__ void wg_sort_group(Scratch& s, Seg seg, BwtShared& sh, Emit emit) {
     seg.start = uniform(seg.start);
     seg.len = uniform(seg.len);
     const int t = threadIdx.x;
@@ -578,8 +591,7 @@ __device__ void wg_sort_group(Scratch& s, Seg seg, BwtShared& sh, Seg* out, uint
                 // group length: walk to the next start (groups are contiguous)
                 uint32_t e = (uint32_t)k + 1;
                 while (e < (uint32_t)m && (K[e] >> kIdxBits) == me) e++;
-                const uint32_t slot = atomicAdd(counter, 1u);
-                out[slot] = Seg{seg.start + (uint32_t)k, e - (uint32_t)k};
+                emit(Seg{seg.start + (uint32_t)k, e - (uint32_t)k});
             }
         }
         carry = carry > tot ? carry : tot;
@@ -650,6 +662,100 @@ __device__ void count_sort_first(const uint8_t* __restrict__ T, int n, uint32_t*
     *ex_out = ex;
 }
 
+// ---- repeat pairs.  A group of two rotations {a, b}, b = a + d (mod n), is a
+// pair of offset d.  Along a repeated passage every (a + m, b + m) is a pair of
+// the same offset, so a and b agree on their first bytes up to the end E of the
+// run of positions a, a+1, .. whose partner offset is d, and their order is the
+// order of the rotations x = E + 1 and y = x + d -- which the labels give
+// whenever x and y lie in different groups (labels are order-consistent at
+// every refinement, and the pairs decided during this pass only refine their
+// own groups).  One pass over the block (partner offsets, run ends) and O(1)
+// per pair replace the log2(repeat length) doubling rounds a long repeated
+// passage costs; pairs whose x, y share a larger group, and every larger
+// group, go on to the doubling (in g2; returns their count, *undecided the
+// pairs among them).
+constexpr uint32_t kNoEnd = 0xffffffffu;
+
+__device__ uint32_t resolve_pairs(int n, Scratch& s, BwtShared& sh, const Seg* g, uint32_t ng, Seg* g2,
+                                  uint32_t* undecided) {
+    const int t = threadIdx.x;
+    uint32_t* pd = s.va;  // partner offset of a pair member, 0 elsewhere
+    uint32_t* ne = s.vb;  // last position of p's run of equal pd (kNoEnd: not in p's wave range)
+    for (int p = t; p < n; p += NT) pd[p] = 0;
+    if (t < 2) sh.cnt[6 + t] = 0;
+    __syncthreads();
+    for (uint32_t q = t; q < ng; q += NT) {
+        const Seg sg = g[q];
+        if (sg.len == 2) {
+            const uint32_t a = s.sa[sg.start], b = s.sa[sg.start + 1];
+            pd[a] = b > a ? b - a : b + n - a;
+            pd[b] = a > b ? a - b : a + n - b;
+        }
+    }
+    __syncthreads();
+    // run ends: wave w scans its range [lo, hi) from the right, 64 positions a step
+    const int w = wave_id(), lane = lane_id();
+    const uint32_t chunk = (((uint32_t)n + NW - 1) / NW + 63u) & ~63u;
+    const uint32_t lo = (uint32_t)w * chunk, hi = min((uint32_t)n, lo + chunk);
+    uint32_t carry = kNoEnd;
+    if (lo < hi) {
+        for (uint32_t ts = lo + ((hi - 1 - lo) & ~63u);; ts -= 64) {
+            const uint32_t p = ts + (uint32_t)lane;
+            const bool valid = p < hi;
+            bool bnd = false;
+            if (valid) {
+                const uint32_t pn = p + 1 == (uint32_t)n ? 0u : p + 1;
+                bnd = pd[p] != pd[pn];
+            }
+            const uint64_t B = __ballot(bnd);
+            const uint64_t above = B & (~0ull << lane);
+            if (valid) ne[p] = above ? ts + (uint32_t)__builtin_ctzll(above) : carry;
+            if (B) carry = ts + (uint32_t)__builtin_ctzll(B);
+            if (ts == lo) break;
+        }
+    }
+    if (lane == 0) sh.wfirst[w] = carry;
+    __syncthreads();
+    for (uint32_t q = t; q < ng; q += NT) {
+        const Seg sg = g[q];
+        bool keep = sg.len != 2;
+        if (!keep) {
+            const uint32_t a = s.sa[sg.start], b = s.sa[sg.start + 1];
+            const uint32_t d = pd[a];
+            uint32_t e = ne[a];
+            if (e == kNoEnd) {  // the run leaves a's wave range: the next range's first end (cyclic)
+                const int wa = (int)(a / chunk);
+                for (int k = 1; k <= NW && e == kNoEnd; ++k) e = sh.wfirst[(wa + k) % NW];
+            }
+            bool a_first;
+            if (e == kNoEnd) {  // every position pairs with offset d = n / 2: equal rotations
+                a_first = a < b;
+            } else {
+                const uint32_t x = e + 1 == (uint32_t)n ? 0u : e + 1;
+                const uint32_t y = x + d >= (uint32_t)n ? x + d - n : x + d;
+                const uint32_t la = s.rank[x], lb = s.rank[y];
+                keep = la == lb;
+                a_first = la < lb;
+            }
+            if (!keep) {
+                const uint32_t f = a_first ? a : b, l = a_first ? b : a;
+                s.sa[sg.start] = f;
+                s.sa[sg.start + 1] = l;
+                s.rank[f] = sg.start;
+                s.rank[l] = sg.start + 1;
+            } else {
+                atomicAdd(&sh.cnt[7], 1u);
+            }
+        }
+        if (keep) g2[atomicAdd(&sh.cnt[6], 1u)] = sg;
+    }
+    __syncthreads();
+    *undecided = uniform(sh.cnt[7]);
+    const uint32_t r = uniform(sh.cnt[6]);
+    __syncthreads();
+    return r;
+}
+
 // ---- labels, phase 2 and the reordered BWT bytes: expects the groups left
 // by phase 1 in s.grp (count sh.cnt[2])
 __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __restrict__ out,
@@ -658,6 +764,16 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
     // ---- labels for phase 2 (only when groups are left): every position is
     // its own label, members of a group carry the group's start
     uint32_t ng = uniform(sh.cnt[2]);
+#ifdef BZ2MI_PHASES
+    const unsigned long long dk0 = wall_clock64();
+    unsigned long long dkp = 0, dkl = 0;
+    uint32_t rounds = 0, first_pass = 1;
+    if (t == 0 && ng > 0) {
+        atomicAdd(&g_dbl_stat[0], 1ull);
+        atomicAdd(&g_dbl_stat[3], (unsigned long long)ng);
+        atomicMax(&g_dbl_stat[10], (unsigned long long)ng);
+    }
+#endif
     if (ng > 0) {
         for (int k = t; k < n; k += NT) s.rank[s.sa[k]] = (uint32_t)k;
         __syncthreads();
@@ -673,11 +789,42 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
         }
         __syncthreads();
     }
+#ifdef BZ2MI_PHASES
+    dkl = wall_clock64() - dk0;
+#endif
     // ---- phase 2: prefix doubling on the unresolved groups
     Seg* g = s.grp;
     Seg* g2 = s.grp2;
     const bool doubled = ng > 0;
+    bool pairs = true;
     for (long long h = 9; ng > 0 && h < n; h <<= 1) {
+        // repeat pairs first (again while the last pass decided some and
+        // enough are left to pay for the block-wide pass)
+#ifdef BZ2MI_PHASES
+        rounds++;
+#endif
+        if (pairs) {
+            uint32_t und;
+#ifdef BZ2MI_PHASES
+            const unsigned long long dp0 = wall_clock64();
+#endif
+            const uint32_t ng2 = resolve_pairs(n, s, sh, g, ng, g2, &und);
+#ifdef BZ2MI_PHASES
+            dkp += wall_clock64() - dp0;
+            if (t == 0 && first_pass) {
+                atomicAdd(&g_dbl_stat[6], (unsigned long long)(ng - ng2));
+                atomicAdd(&g_dbl_stat[7], (unsigned long long)und);
+                atomicAdd(&g_dbl_stat[8], (unsigned long long)ng2);
+            }
+            first_pass = 0;
+#endif
+            pairs = ng2 < ng && und > 64;
+            ng = ng2;
+            Seg* tg = g;
+            g = g2;
+            g2 = tg;
+            if (ng == 0) break;
+        }
         // pass A: snapshot keys label[i+h] for every member of every group
         if (t == 0) sh.cnt[4] = 0;
         __syncthreads();
@@ -702,7 +849,8 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
         __syncthreads();
         for (uint32_t q = 0; q < ng; ++q) {
             const Seg sg = g[q];
-            if (uniform(sg.len) > (uint32_t)kSmall) wg_sort_group(s, sg, sh, g2, &sh.cnt[5]);
+            if (uniform(sg.len) > (uint32_t)kSmall)
+                wg_sort_group(s, sg, sh, [&](Seg o) { g2[atomicAdd(&sh.cnt[5], 1u)] = o; });
         }
         __syncthreads();
         for (;;) {
@@ -721,6 +869,17 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
         __syncthreads();
     }
     BZ2MI_PHASE(g_bwt_phase, 4, stamp);
+#ifdef BZ2MI_PHASES
+    if (t == 0 && doubled) {
+        const unsigned long long dt = wall_clock64() - dk0;
+        atomicAdd(&g_dbl_stat[1], dt);
+        atomicMax(&g_dbl_stat[2], dt);
+        atomicAdd(&g_dbl_stat[4], (unsigned long long)rounds);
+        atomicMax(&g_dbl_stat[5], (unsigned long long)rounds);
+        atomicAdd(&g_dbl_stat[11], dkp);
+        atomicAdd(&g_dbl_stat[12], dkl);
+    }
+#endif
     // ---- BWT bytes and origPtr of the positions phase 2 reordered (phase 1
     // wrote the others as it placed them); 4 positions per thread and step
     if (doubled) {
@@ -3715,11 +3874,12 @@ __global__ void redo_all_kernel(uint32_t* redo, int nblocks) {
     if (b < nblocks && redo[b] == 1u) redo[b] = 2u;
 }
 
-// ---- kernel 4 (one launch per round, one workgroup per block): the block's
-// tie groups sorted by their next 8 bytes -- groups of <= kTieThread
-// rotations one per thread, larger ones one per wave.  New ties go to the
-// next round's list; the last round hands them to the block's group list for
-// prefix doubling.
+// ---- kernel 4 (one launch per round, gridDim.y workgroups per block, each
+// a slice of its list): the block's tie groups sorted by their next 8 bytes
+// -- groups of <= kTieThread rotations one per thread, larger ones one per
+// wave.  New ties go to the next round's list (tout_count zeroed before the
+// launch); the last round hands them to the block's group list for prefix
+// doubling.
 __global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict__ blocks, size_t stride,
                                                       const uint32_t* __restrict__ lens,
                                                       uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
@@ -3731,15 +3891,10 @@ __global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict_
                                                       uint32_t* __restrict__ ngroups, uint32_t* __restrict__ p2list,
                                                       uint32_t* __restrict__ p2count, int last) {
     __shared__ TieLds L;
-    __shared__ uint32_t ocount;
     const uint32_t b = blockIdx.x;
     const uint32_t nq = uniform(tin_count[b]);
-    if (nq == 0) {
-        if (threadIdx.x == 0) tout_count[b] = 0;
-        return;
-    }
-    if (threadIdx.x == 0) ocount = 0;
-    __syncthreads();
+    const uint32_t y0 = blockIdx.y * NT, ystep = gridDim.y * NT;
+    if (y0 >= nq) return;
     const int n = (int)uniform(lens[b]);
     const uint8_t* T = blocks + (size_t)b * stride;
     uint32_t* sa = sa_all + (size_t)b * stride;
@@ -3747,7 +3902,8 @@ __global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict_
     const uint64_t* in = tin + (size_t)b * tcap;
     const GroupSink sink = last ? GroupSink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu,
                                             p2list, p2count, b, nullptr, nullptr}
-                                : GroupSink{nullptr, nullptr, 0, nullptr, nullptr, b, tout + (size_t)b * tcap, &ocount};
+                                : GroupSink{nullptr, nullptr, 0, nullptr, nullptr, b, tout + (size_t)b * tcap,
+                                            &tout_count[b]};
     auto unpack = [](uint64_t e, Seg& seg, uint32_t& d) {
         seg = Seg{(uint32_t)(e >> 22) & 0xfffffu, ((uint32_t)(e >> 13) & 511u) + 1u};
         d = (uint32_t)e & 0x1fffu;
@@ -3755,7 +3911,7 @@ __global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict_
     // small groups: one per thread, 256 at a time; their members are loaded
     // by all threads at once (flattened) into LDS, then every thread ranks
     // its own group there
-    for (uint32_t q0 = 0; q0 < nq; q0 += NT) {
+    for (uint32_t q0 = y0; q0 < nq; q0 += ystep) {
         const uint32_t q = q0 + threadIdx.x;
         uint32_t d = 0;
         Seg seg{0, 0};
@@ -3807,7 +3963,7 @@ __global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict_
         __syncthreads();
     }
     // large groups: one per wave (the list is scanned for them)
-    for (uint32_t q0 = wave_id() * 64; q0 < nq; q0 += NT) {
+    for (uint32_t q0 = y0 + wave_id() * 64; q0 < nq; q0 += ystep) {
         const uint32_t q = q0 + lane_id();
         uint32_t d = 0;
         Seg seg{0, 0};
@@ -3823,8 +3979,6 @@ __global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict_
             wave_sort_any<0>(T, n, s, sg, dd, sink, bw, orig_out + b);
         }
     }
-    __syncthreads();
-    if (threadIdx.x == 0 && !last) tout_count[b] = ocount;
 }
 
 // ---- kernel 5: blocks with groups left: labels, prefix doubling, BWT bytes
@@ -3855,6 +4009,532 @@ __global__ __launch_bounds__(256) void bwt_double_kernel(const uint8_t* __restri
         bwt_finish(blocks + (size_t)b * stride, n, bwt_out + (size_t)b * stride, orig_out + b, s, sh,
                    b == nblocks / 2);
         __syncthreads();
+    }
+}
+
+// ==== prefix doubling over the whole grid (blocks beyond kBwtLdsText) ====
+// Every group of every enlisted block sits in one flat list; each round is a
+// few launches over all of them, so a block's doubling is spread over the
+// chip instead of one workgroup (a 900 KB block of text with long repeated
+// passages keeps ~50,000 groups for ~10 rounds: one workgroup per block left
+// the double stage latency-bound at ~0.1-0.3 s per block).  Round r, h = 9 << r:
+//   pairset / runend / decide  the repeat pairs of resolve_pairs, grid-wide
+//                              (partner offsets tagged with the round, so the
+//                              array is never cleared between rounds);
+//   snap                       key[i] = label[i + h] << 20 | i for every member
+//                              of every group (all reads before any relabel);
+//   sort                       groups of 2 and <= 8 by one thread (ranks by
+//                              counting), <= 512 by one wave (register bitonic),
+//   large                      larger ones by one workgroup (LSD radix);
+// subgroups go to the next round's lists.  Then the BWT bytes of the enlisted
+// blocks.  Launches with nothing to do return at once (counters in G.ctr).
+struct DblSlot {
+    uint64_t* ka;
+    uint64_t* kb;
+    uint32_t* rank;
+    uint32_t* pd;
+    uint32_t* ne;
+    uint32_t* va;  // radix values of large groups
+    uint32_t* vb;
+    uint32_t* cf;
+};
+
+__device__ __forceinline__ DblSlot dbl_slot(const DblGrid& G, uint32_t k) {
+    const size_t S = (size_t)G.S;
+    uint8_t* p = G.scratch + (size_t)k * G.per_slot;
+    DblSlot d;
+    d.ka = (uint64_t*)p; p += 8 * S;
+    d.kb = (uint64_t*)p; p += 8 * S;
+    d.rank = (uint32_t*)p; p += 4 * S;
+    d.pd = (uint32_t*)p; p += 4 * S;
+    d.ne = (uint32_t*)p; p += 4 * S;
+    d.va = (uint32_t*)p; p += 4 * S;
+    d.vb = (uint32_t*)p; p += 4 * S;
+    d.cf = (uint32_t*)p;
+    return d;
+}
+
+__device__ __forceinline__ void dbl_unpack(uint64_t e, uint32_t& k, uint32_t& start, uint32_t& len) {
+    k = (uint32_t)(e >> 42);
+    start = (uint32_t)(e >> 22) & 0xfffffu;
+    len = ((uint32_t)(e >> 13) & 511u) + 1u;
+}
+__device__ __forceinline__ uint64_t dbl_large_pack(uint32_t k, uint32_t start, uint32_t len) {
+    return ((uint64_t)k << 40) | ((uint64_t)start << 20) | len;
+}
+
+// wave-aggregated append (every lane of the wave that reaches it calls it)
+__device__ __forceinline__ void dbl_append(bool want, uint64_t e, uint64_t* list, uint32_t* cnt) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (want) list[base + (uint32_t)__popcll(m & __lanemask_lt())] = e;
+}
+
+// list appends staged in LDS and written with one global atomic per workgroup
+// and step (the chip-wide list counters are single addresses)
+constexpr int kDblStage = 2048;
+struct DblOut {
+    uint64_t buf[kDblStage];
+    uint32_t n, nn, base;
+    uint32_t cnt[2];
+};
+__device__ __forceinline__ void stage_push(DblOut& o, bool want, uint64_t e) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(&o.n, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (want) o.buf[base + (uint32_t)__popcll(m & __lanemask_lt())] = e;
+}
+// every thread of the workgroup calls it
+__device__ __forceinline__ void stage_flush(DblOut& o, uint64_t* list, uint32_t* cnt) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        o.nn = o.n;
+        o.base = o.n ? atomicAdd(cnt, o.n) : 0u;
+        o.n = 0;
+    }
+    __syncthreads();
+    const uint32_t nn = o.nn, bb = o.base;
+    for (uint32_t j = threadIdx.x; j < nn; j += NT) list[bb + j] = o.buf[j];
+    __syncthreads();
+}
+
+// partner offsets and run ends recomputed in round r (c[6]): round 0 always;
+// later while the last recomputation decided at least a ninth of its pairs.
+// c[7] = 1 + the round they were last recomputed in (their tag); pairs still
+// undecided keep their run end (a fact about the text), so every round
+// re-checks the two rotations after it as the labels refine.
+__device__ __forceinline__ bool dbl_pairs_on(const uint32_t* ctr, int r) {
+    if (r == 0) return true;
+    const uint32_t* c = ctr + kDblCtr * (r - 1);
+    return c[6] != 0 && c[4] > 0 && c[3] >= c[4] / 8;
+}
+
+// the wave's first list index and the stride of a grid-wide wave loop
+__device__ __forceinline__ uint32_t dbl_wave_base() { return (blockIdx.x * NW + (uint32_t)wave_id()) * 64u; }
+__device__ __forceinline__ uint32_t dbl_wave_stride() { return gridDim.x * NW * 64u; }
+
+// labels: every position its SA index (group members get their group's start
+// next); partner offsets cleared
+__global__ __launch_bounds__(256) void dbl_init_rank_kernel(DblGrid G) {
+    const uint32_t P = *G.p2count;
+    const uint32_t C = ((uint32_t)G.S + 4095u) / 4096u;
+    for (uint32_t it = blockIdx.x; it < P * C; it += gridDim.x) {
+        const uint32_t k = it / C, c = it - k * C;
+        const uint32_t b = G.p2list[k];
+        const uint32_t n = G.lens[b];
+        const uint32_t lo = c * 4096u;
+        if (lo >= n) continue;
+        const uint32_t hi = min(n, lo + 4096u);
+        const uint32_t* sa = G.sa_all + (size_t)b * G.stride;
+        const DblSlot d = dbl_slot(G, k);
+        uint32_t iv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t p = lo + (uint32_t)j * NT + threadIdx.x;
+            iv[j] = p < hi ? sa[p] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t p = lo + (uint32_t)j * NT + threadIdx.x;
+            if (p < hi) {
+                d.rank[iv[j]] = p;
+                d.pd[p] = 0;
+            }
+        }
+    }
+}
+
+// group labels; the phase-1 group lists become the round-0 lists
+__global__ __launch_bounds__(256) void dbl_init_groups_kernel(DblGrid G) {
+    __shared__ DblOut o;
+    if (threadIdx.x == 0) o.n = 0;
+    __syncthreads();
+    const uint32_t P = *G.p2count;
+    for (uint32_t k = blockIdx.x; k < P; k += gridDim.x) {
+        const uint32_t b = G.p2list[k];
+        const uint32_t ng = G.ngroups[b];
+        const Seg* grp = G.grp_all + (size_t)b * bwt_group_stride(G.stride);
+        const uint32_t* sa = G.sa_all + (size_t)b * G.stride;
+        const DblSlot d = dbl_slot(G, k);
+        for (uint32_t q0 = 0; q0 < ng; q0 += NT) {
+            const uint32_t q = q0 + threadIdx.x;
+            Seg sg{0, 0};
+            if (q < ng) sg = grp[q];
+            if (sg.len <= 64)
+                for (uint32_t j = 0; j < sg.len; ++j) d.rank[sa[sg.start + j]] = sg.start;
+            uint64_t big = __ballot(sg.len > 64);
+            while (big) {
+                const int l = __builtin_ctzll(big);
+                big &= big - 1;
+                const uint32_t st = uniform((uint32_t)__shfl((int)sg.start, l));
+                const uint32_t ln = uniform((uint32_t)__shfl((int)sg.len, l));
+                for (uint32_t j = lane_id(); j < ln; j += 64) d.rank[sa[st + j]] = st;
+            }
+            stage_push(o, q < ng && sg.len <= (uint32_t)kSmall, sq_pack(k, sg.start, max(sg.len, 1u), 0));
+            stage_flush(o, G.list[0], &G.ctr[0]);
+            dbl_append(q < ng && sg.len > (uint32_t)kSmall, dbl_large_pack(k, sg.start, sg.len), G.large[0],
+                       &G.ctr[2]);
+        }
+    }
+}
+
+// partner offsets of the round's pairs, tagged with the round
+__global__ __launch_bounds__(256) void dbl_pairset_kernel(DblGrid G, int r) {
+    const bool on = dbl_pairs_on(G.ctr, r);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        G.ctr[kDblCtr * r + 6] = on ? 1u : 0u;
+        G.ctr[kDblCtr * r + 7] = on ? (uint32_t)(r + 1) : r ? G.ctr[kDblCtr * (r - 1) + 7] : 0u;
+    }
+    if (!on) return;
+    const uint32_t cin = G.ctr[kDblCtr * r];
+    const uint32_t tag = (uint32_t)(r + 1) << 20;
+    const uint64_t* list = G.list[0];
+    for (uint32_t q = blockIdx.x * NT + threadIdx.x; q < cin; q += gridDim.x * NT) {
+        uint32_t k, start, len;
+        dbl_unpack(list[q], k, start, len);
+        if (len != 2) continue;
+        const uint32_t b = G.p2list[k];
+        const uint32_t n = G.lens[b];
+        const uint32_t* sa = G.sa_all + (size_t)b * G.stride;
+        const uint32_t a = sa[start], c = sa[start + 1];
+        const DblSlot d = dbl_slot(G, k);
+        d.pd[a] = tag | (c > a ? c - a : c + n - a);
+        d.pd[c] = tag | (a > c ? a - c : a + n - c);
+    }
+}
+
+// run ends of equal partner offsets: wave w of chunk c scans the 1024
+// positions of sub-range 4c + w from the right (cf = its first run end)
+__global__ __launch_bounds__(256) void dbl_runend_kernel(DblGrid G, int r) {
+    if (G.ctr[kDblCtr * r + 6] == 0) return;
+    const uint32_t P = *G.p2count;
+    const uint32_t C = ((uint32_t)G.S + 4095u) / 4096u;
+    const int w = wave_id(), lane = lane_id();
+    for (uint32_t it = blockIdx.x; it < P * C; it += gridDim.x) {
+        const uint32_t k = it / C, c = it - k * C;
+        const uint32_t b = G.p2list[k];
+        const uint32_t n = G.lens[b];
+        const uint32_t lo = c * 4096u + (uint32_t)w * 1024u;
+        const DblSlot d = dbl_slot(G, k);
+        if (lo >= n) {
+            if (lane == 0) d.cf[c * 4 + w] = kNoEnd;
+            continue;
+        }
+        const uint32_t hi = min(n, lo + 1024u);
+        uint32_t carry = kNoEnd;
+        for (uint32_t ts = lo + ((hi - 1 - lo) & ~63u);; ts -= 64) {
+            const uint32_t p = ts + (uint32_t)lane;
+            const bool valid = p < hi;
+            bool bnd = false;
+            if (valid) bnd = d.pd[p] != d.pd[p + 1 == n ? 0u : p + 1];
+            const uint64_t B = __ballot(bnd);
+            const uint64_t above = B & (~0ull << lane);
+            if (valid) d.ne[p] = above ? ts + (uint32_t)__builtin_ctzll(above) : carry;
+            if (B) carry = ts + (uint32_t)__builtin_ctzll(B);
+            if (ts == lo) break;
+        }
+        if (lane == 0) d.cf[c * 4 + w] = carry;
+    }
+}
+
+// pairs decided by the rotations after their run (resolve_pairs); the rest of
+// the round's groups (blocks with h < n) go on to the other list
+__global__ __launch_bounds__(256) void dbl_decide_kernel(DblGrid G, int r) {
+    __shared__ DblOut o;
+    uint32_t* cnt = G.ctr + kDblCtr * r;
+    const uint32_t tag = cnt[7] << 20;  // the last recomputation's tag (0: none)
+    const uint32_t cin = cnt[0];
+    const uint32_t h = 9u << r;
+    const int t = threadIdx.x;
+    if (t == 0) {
+        o.n = 0;
+        o.cnt[0] = o.cnt[1] = 0;
+    }
+    __syncthreads();
+    const uint64_t* lin = G.list[0];
+    uint64_t* lout = G.list[1];
+    uint32_t ndec = 0, nund = 0;
+    for (uint32_t q0 = blockIdx.x * NT; q0 < cin; q0 += gridDim.x * NT) {
+        const uint32_t q = q0 + (uint32_t)t;
+        bool keep = false;
+        uint64_t e = 0;
+        if (q < cin) {
+            e = lin[q];
+            uint32_t k, start, len;
+            dbl_unpack(e, k, start, len);
+            const uint32_t b = G.p2list[k];
+            const uint32_t n = G.lens[b];
+            keep = h < n;
+            uint32_t* sa = G.sa_all + (size_t)b * G.stride;
+            const DblSlot d = dbl_slot(G, k);
+            uint32_t a = 0, c = 0, off = 0;
+            if (keep && len == 2 && tag) {
+                a = sa[start];
+                c = sa[start + 1];
+                off = c > a ? c - a : c + n - a;
+            }
+            // a run end only where the pair was a pair at the last recomputation
+            if (keep && len == 2 && tag && d.pd[a] == (tag | off)) {
+                uint32_t end = d.ne[a];
+                if (end == kNoEnd) {  // the run leaves a's sub-range: the next sub-range's first end (cyclic)
+                    const uint32_t nsub = (n + 1023u) / 1024u;
+                    uint32_t sj = a / 1024u;
+                    for (uint32_t j = 0; j < nsub && end == kNoEnd; ++j) {
+                        sj = sj + 1 == nsub ? 0u : sj + 1;
+                        end = d.cf[sj];
+                    }
+                }
+                bool a_first = a < c;  // no end anywhere: every position pairs at n / 2, equal rotations
+                bool dec = true;
+                if (end != kNoEnd) {
+                    const uint32_t x = end + 1 == n ? 0u : end + 1;
+                    const uint32_t y = x + off >= n ? x + off - n : x + off;
+                    const uint32_t la = d.rank[x], lb = d.rank[y];
+                    dec = la != lb;
+                    a_first = la < lb;
+                }
+                if (dec) {
+                    const uint32_t f = a_first ? a : c, l = a_first ? c : a;
+                    sa[start] = f;
+                    sa[start + 1] = l;
+                    d.rank[f] = start;
+                    d.rank[l] = start + 1;
+                    keep = false;
+                    ndec++;
+                } else {
+                    nund++;
+                }
+            }
+        }
+        stage_push(o, keep, e);
+        stage_flush(o, lout, &cnt[1]);
+    }
+    atomicAdd(&o.cnt[0], ndec);
+    atomicAdd(&o.cnt[1], nund);
+    __syncthreads();
+    if (t == 0) {
+        if (o.cnt[0]) atomicAdd(&cnt[3], o.cnt[0]);
+        if (o.cnt[1]) atomicAdd(&cnt[4], o.cnt[1]);
+    }
+}
+
+// keys of every member of the round's groups, before any relabelling
+__global__ __launch_bounds__(256) void dbl_snap_kernel(DblGrid G, int r) {
+    const uint32_t* cnt = G.ctr + kDblCtr * r;
+    const uint32_t c1 = cnt[1];
+    const uint64_t* lmid = G.list[1];
+    const uint32_t cl = cnt[2];
+    const uint32_t h = 9u << r;
+    const int lane = lane_id();
+    for (uint32_t q0 = dbl_wave_base(); q0 < c1; q0 += dbl_wave_stride()) {
+        const uint32_t q = q0 + (uint32_t)lane;
+        uint32_t k = 0, start = 0, len = 0;
+        if (q < c1) {
+            dbl_unpack(lmid[q], k, start, len);
+            if (h >= G.lens[G.p2list[k]]) len = 0;
+        }
+        if (len > 0 && len <= 32) {
+            const uint32_t b = G.p2list[k];
+            const uint32_t n = G.lens[b];
+            const uint32_t* sa = G.sa_all + (size_t)b * G.stride;
+            const DblSlot d = dbl_slot(G, k);
+            for (uint32_t j = 0; j < len; ++j) {
+                const uint32_t i = sa[start + j];
+                const uint32_t ih = i + h >= n ? i + h - n : i + h;
+                d.ka[start + j] = ((uint64_t)d.rank[ih] << kIdxBits) | i;
+            }
+        }
+        uint64_t big = __ballot(len > 32);
+        while (big) {
+            const int l = __builtin_ctzll(big);
+            big &= big - 1;
+            const uint32_t kk = uniform((uint32_t)__shfl((int)k, l));
+            const uint32_t st = uniform((uint32_t)__shfl((int)start, l));
+            const uint32_t ln = uniform((uint32_t)__shfl((int)len, l));
+            const uint32_t b = G.p2list[kk];
+            const uint32_t n = G.lens[b];
+            const uint32_t* sa = G.sa_all + (size_t)b * G.stride;
+            const DblSlot d = dbl_slot(G, kk);
+            for (uint32_t j = (uint32_t)lane; j < ln; j += 64) {
+                const uint32_t i = sa[st + j];
+                const uint32_t ih = i + h >= n ? i + h - n : i + h;
+                d.ka[st + j] = ((uint64_t)d.rank[ih] << kIdxBits) | i;
+            }
+        }
+    }
+    for (uint32_t q = blockIdx.x; q < cl; q += gridDim.x) {
+        const uint64_t e = G.large[r & 1][q];
+        const uint32_t k = (uint32_t)(e >> 40), st = (uint32_t)(e >> 20) & 0xfffffu, ln = (uint32_t)e & 0xfffffu;
+        const uint32_t b = G.p2list[k];
+        const uint32_t n = G.lens[b];
+        if (h >= n) continue;
+        const uint32_t* sa = G.sa_all + (size_t)b * G.stride;
+        const DblSlot d = dbl_slot(G, k);
+        for (uint32_t j = threadIdx.x; j < ln; j += NT) {
+            const uint32_t i = sa[st + j];
+            const uint32_t ih = i + h >= n ? i + h - n : i + h;
+            d.ka[st + j] = ((uint64_t)d.rank[ih] << kIdxBits) | i;
+        }
+    }
+}
+
+constexpr int kDblThread = 8;  // groups a thread sorts by counting
+
+// groups of <= 512: sorted on their keys, relabelled, subgroups to the next
+// round's list
+__global__ __launch_bounds__(256) void dbl_sort_kernel(DblGrid G, int r) {
+    __shared__ DblOut o;
+    const uint32_t c1 = G.ctr[kDblCtr * r + 1];
+    const uint64_t* lmid = G.list[1];
+    uint64_t* lnext = G.list[0];
+    uint32_t* nxt = G.ctr + kDblCtr * (r + 1);
+    const uint32_t h = 9u << r;
+    const int t = threadIdx.x;
+    if (t == 0) o.n = 0;
+    __syncthreads();
+    for (uint32_t q0 = blockIdx.x * NT; q0 < c1; q0 += gridDim.x * NT) {
+        const uint32_t q = q0 + (uint32_t)t;
+        uint32_t k = 0, start = 0, len = 0;
+        if (q < c1) {
+            dbl_unpack(lmid[q], k, start, len);
+            if (h >= G.lens[G.p2list[k]]) len = 0;
+        }
+        const bool thr = len > 0 && len <= (uint32_t)kDblThread;
+        uint32_t* sa = nullptr;
+        DblSlot d{};
+        if (thr) {
+            sa = G.sa_all + (size_t)G.p2list[k] * G.stride;
+            d = dbl_slot(G, k);
+        }
+        bool pair_tie = false;
+        if (thr && len == 2) {
+            const uint64_t x = d.ka[start], y = d.ka[start + 1];
+            const uint64_t f = x < y ? x : y, l = x < y ? y : x;
+            const uint32_t fi = (uint32_t)f & ((1u << kIdxBits) - 1u), li = (uint32_t)l & ((1u << kIdxBits) - 1u);
+            pair_tie = (f >> kIdxBits) == (l >> kIdxBits);
+            sa[start] = fi;
+            sa[start + 1] = li;
+            d.rank[fi] = start;
+            d.rank[li] = pair_tie ? start : start + 1;
+        }
+        stage_push(o, pair_tie, sq_pack(k, start, 2, 0));
+        const bool cnt_sort = thr && len > 2;
+        if (__ballot(cnt_sort)) {
+            uint64_t kk[kDblThread];
+#pragma unroll
+            for (int j = 0; j < kDblThread; ++j) kk[j] = cnt_sort && (uint32_t)j < len ? d.ka[start + j] : ~0ull;
+#pragma unroll
+            for (int j = 0; j < kDblThread; ++j) {
+                bool want = false;
+                uint64_t ent = 0;
+                if (cnt_sort && (uint32_t)j < len) {
+                    const uint64_t kj = kk[j], gj = kj >> kIdxBits;
+                    uint32_t pos = 0, lbl = 0, eq = 0;
+#pragma unroll
+                    for (int m = 0; m < kDblThread; ++m) {
+                        pos += kk[m] < kj;
+                        lbl += (kk[m] >> kIdxBits) < gj;
+                        eq += (kk[m] >> kIdxBits) == gj;
+                    }
+                    const uint32_t i = (uint32_t)kj & ((1u << kIdxBits) - 1u);
+                    sa[start + pos] = i;
+                    d.rank[i] = start + lbl;
+                    want = eq >= 2 && pos == lbl;
+                    ent = sq_pack(k, start + lbl, max(eq, 1u), 0);
+                }
+                stage_push(o, want, ent);
+            }
+        }
+        uint64_t big = __ballot(len > (uint32_t)kDblThread);
+        while (big) {
+            const int l = __builtin_ctzll(big);
+            big &= big - 1;
+            const uint32_t kw = uniform((uint32_t)__shfl((int)k, l));
+            const uint32_t st = uniform((uint32_t)__shfl((int)start, l));
+            const uint32_t ln = uniform((uint32_t)__shfl((int)len, l));
+            const uint32_t b = G.p2list[kw];
+            const DblSlot dw = dbl_slot(G, kw);
+            Scratch s{};
+            s.sa = G.sa_all + (size_t)b * G.stride;
+            s.rank = dw.rank;
+            s.ka = dw.ka;
+            const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, kw, lnext, &nxt[0], nullptr};
+            wave_sort_any<1>(nullptr, (int)G.lens[b], s, Seg{st, ln}, 0, sink, nullptr, nullptr);
+        }
+        stage_flush(o, lnext, &nxt[0]);
+    }
+}
+
+// groups of > 512: one workgroup each
+__global__ __launch_bounds__(256) void dbl_large_kernel(DblGrid G, int r) {
+    __shared__ BwtShared sh;
+    const uint32_t cl = G.ctr[kDblCtr * r + 2];
+    uint32_t* nxt = G.ctr + kDblCtr * (r + 1);
+    const uint32_t h = 9u << r;
+    for (uint32_t q = blockIdx.x; q < cl; q += gridDim.x) {
+        const uint64_t e = G.large[r & 1][q];
+        const uint32_t k = (uint32_t)(e >> 40), st = (uint32_t)(e >> 20) & 0xfffffu, ln = (uint32_t)e & 0xfffffu;
+        const uint32_t b = G.p2list[k];
+        if (h >= G.lens[b]) continue;
+        const DblSlot d = dbl_slot(G, k);
+        Scratch s{};
+        s.sa = G.sa_all + (size_t)b * G.stride;
+        s.rank = d.rank;
+        s.ka = d.ka;
+        s.kb = d.kb;
+        s.va = d.va;
+        s.vb = d.vb;
+        uint64_t* lnext = G.large[(r + 1) & 1];
+        uint64_t* list0 = G.list[0];
+        wg_sort_group(s, Seg{st, ln}, sh, [&](Seg o) {
+            if (o.len <= (uint32_t)kSmall) list0[atomicAdd(&nxt[0], 1u)] = sq_pack(k, o.start, o.len, 0);
+            else lnext[atomicAdd(&nxt[2], 1u)] = dbl_large_pack(k, o.start, o.len);
+        });
+        __syncthreads();
+    }
+}
+
+// BWT bytes and origPtr of the positions the doubling may have moved: the
+// members of the phase-1 groups (phase 1 wrote every other position's byte)
+__device__ __forceinline__ void dbl_emit_one(const uint8_t* T, uint32_t n, const uint32_t* sa, uint8_t* out,
+                                             uint32_t* orig, uint32_t p) {
+    const uint32_t i = sa[p];
+    out[p] = bwt_byte(T, (int)n, i);
+    if (i == 0) *orig = p;
+}
+__global__ __launch_bounds__(256) void dbl_emit_kernel(DblGrid G) {
+    const uint32_t P = *G.p2count;
+    for (uint32_t k = blockIdx.x; k < P; k += gridDim.x) {
+        const uint32_t b = G.p2list[k];
+        const uint32_t n = G.lens[b];
+        const uint32_t ng = G.ngroups[b];
+        const Seg* grp = G.grp_all + (size_t)b * bwt_group_stride(G.stride);
+        const uint32_t* sa = G.sa_all + (size_t)b * G.stride;
+        const uint8_t* T = G.blocks + (size_t)b * G.stride;
+        uint8_t* out = G.bwt_out + (size_t)b * G.stride;
+        uint32_t* orig = G.orig_out + b;
+        for (uint32_t q0 = 0; q0 < ng; q0 += NT) {
+            const uint32_t q = q0 + threadIdx.x;
+            Seg sg{0, 0};
+            if (q < ng) sg = grp[q];
+            if (sg.len <= 64)
+                for (uint32_t j = 0; j < sg.len; ++j) dbl_emit_one(T, n, sa, out, orig, sg.start + j);
+            uint64_t big = __ballot(sg.len > 64);
+            while (big) {
+                const int l = __builtin_ctzll(big);
+                big &= big - 1;
+                const uint32_t st = uniform((uint32_t)__shfl((int)sg.start, l));
+                const uint32_t ln = uniform((uint32_t)__shfl((int)sg.len, l));
+                for (uint32_t j = lane_id(); j < ln; j += 64) dbl_emit_one(T, n, sa, out, orig, st + j);
+            }
+        }
     }
 }
 

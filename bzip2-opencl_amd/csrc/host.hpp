@@ -138,6 +138,11 @@ struct bz2mi_ctx {
     int wlevel_grid = 0;                            // resident workgroups of bwt_wlevel_kernel
     uint32_t* d_lspill = nullptr;                   // wave-level stage spill (one word per rotation of a batch)
     uint32_t* d_scb = nullptr;                      // per-block small-batch counts (LDS-text path)
+    // grid-wide prefix doubling (blocks beyond kBwtLdsText): slots, group lists, counters
+    uint8_t* d_dscratch = nullptr;
+    uint64_t* d_dlist[2] = {nullptr, nullptr};
+    uint64_t* d_dlarge[2] = {nullptr, nullptr};
+    uint32_t* d_dctr = nullptr;
     int bwtq_blocks = 0;           // capacity of the queues in blocks
     uint32_t* d_state = nullptr;   // p x 258 persistent seed sums (H4)
     uint32_t* d_crctab = nullptr;

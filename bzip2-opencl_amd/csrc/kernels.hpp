@@ -71,6 +71,10 @@ __global__ void bwt_small_kernel(const uint8_t* blocks, size_t stride, const uin
                                  uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* squeue,
                                  const uint32_t* scount, size_t scap, uint64_t* tl, uint32_t* tcount, size_t tcap);
 constexpr int kBwtTieRounds = 6;  // rounds of 8 more bytes for tie groups before prefix doubling
+#ifndef BZ2MI_AB_TIE_ROUNDS_GRID
+#define BZ2MI_AB_TIE_ROUNDS_GRID 3
+#endif
+constexpr int kBwtTieRoundsGrid = BZ2MI_AB_TIE_ROUNDS_GRID;  // ... before the grid-wide doubling
 __global__ void bwt_tie_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* tin, const uint32_t* tin_count,
                                uint64_t* tout, uint32_t* tout_count, size_t tcap, BwtSeg* grp_all,
@@ -80,6 +84,52 @@ __global__ void bwt_double_kernel(const uint8_t* blocks, size_t stride, const ui
                                   uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch,
                                   size_t scratch_per_slot, int S, BwtSeg* grp_all, const uint32_t* ngroups,
                                   const uint32_t* p2list, const uint32_t* p2count, uint32_t* pull);
+// Blocks beyond kBwtLdsText: prefix doubling over the whole grid, one launch
+// per step and round (dbl_* kernels, bwt.hip), every group of every block of
+// the batch in one flat list.  Per enlisted block (slot k = its p2list index)
+// a scratch slot of dbl_slot_bytes(S); lists of dbl_list_cap(S) entries per slot.
+struct DblGrid {
+    const uint8_t* blocks;
+    size_t stride;
+    const uint32_t* lens;
+    uint32_t* sa_all;
+    uint8_t* bwt_out;
+    uint32_t* orig_out;
+    const BwtSeg* grp_all;
+    const uint32_t* ngroups;
+    const uint32_t* p2list;
+    const uint32_t* p2count;
+    uint8_t* scratch;
+    size_t per_slot;
+    int S;
+    uint64_t* list[2];   // groups of <= 512 rotations (sq_pack entries, block field = slot)
+    uint64_t* large[2];  // larger groups: slot << 40 | start << 20 | len
+    uint32_t* ctr;       // kDblCtr counters per round (zeroed before the first launch)
+};
+constexpr int kDblCtr = 8;
+constexpr int kDblMaxRounds = 20;  // 9 << 19 > 2^20 >= S
+inline size_t dbl_slot_bytes(int S) {
+    const size_t s = (size_t)S;
+    return (36 * s + 4 * (s / 1024 + 8) + 255) & ~(size_t)255;
+}
+inline size_t dbl_list_cap(int S) { return (size_t)S / 2 + 2; }
+inline size_t dbl_large_cap(int S) { return (size_t)S / 513 + 2; }
+// rounds of the doubling for blocks of <= S bytes (h = 9 << r while h < S)
+inline int dbl_rounds(int S) {
+    int r = 0;
+    while (r < kDblMaxRounds && (9ll << r) < (long long)S) ++r;
+    return r;
+}
+__global__ void dbl_init_rank_kernel(DblGrid G);
+__global__ void dbl_init_groups_kernel(DblGrid G);
+__global__ void dbl_pairset_kernel(DblGrid G, int r);
+__global__ void dbl_runend_kernel(DblGrid G, int r);
+__global__ void dbl_decide_kernel(DblGrid G, int r);
+__global__ void dbl_snap_kernel(DblGrid G, int r);
+__global__ void dbl_sort_kernel(DblGrid G, int r);
+__global__ void dbl_large_kernel(DblGrid G, int r);
+__global__ void dbl_emit_kernel(DblGrid G);
+
 // small-queue capacity (entries) per block and level-queue capacity per block
 // (a shard holds the entries of every 64th block)
 __host__ __device__ inline size_t bwt_squeue_per_block(int S) { return (size_t)S / 2 + 2; }
@@ -105,6 +155,7 @@ int mtf_phases(unsigned long long* out);
 int fe_phases(unsigned long long* out);
 int tbk_stats(unsigned long long* out);
 int tbk_resolve_stats(unsigned long long* out);
+int dbl_stats(unsigned long long* out);
 int tbk_trace(void* host_mapped);
 int run_selftest(uint32_t* host_bad, int n);  // cross-lane primitive checks
 int huffman_threads();  // workgroup size of huffman_kernel
