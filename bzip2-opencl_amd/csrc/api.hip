@@ -197,9 +197,15 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
                                c->d_tq[0], tc[0], tcap, t.d_redo, mode, c->d_sq, c->d_scb, tcap);
         }
     } else {
+        // mid-size first-byte buckets listed in the second tie list (free
+        // until the tie rounds), sorted whole by bwt_bigbucket_kernel
         hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
                            t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap,
-                           t.d_present);
+                           t.d_present, c->d_tq[1], tc[1], tcap);
+        HIPCHECK(hipGetLastError());
+        hipLaunchKernelGGL(bwt_bigbucket_kernel, dim3(nb, 256), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
+                           t.d_sa, t.d_bwt, t.d_orig, c->d_tq[1], tc[1], tcap, c->d_tq[0], tc[0], tcap, c->d_lq[0],
+                           lcount + 2 * kBwtShards, lcap);
     }
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");

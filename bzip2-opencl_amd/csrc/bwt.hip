@@ -918,6 +918,7 @@ __device__ void bwt_finish(const uint8_t* __restrict__ T, int n, uint8_t* __rest
 //     sort of their own;
 // all from LDS.  Tie groups go to the sink with their depth.
 constexpr int kSub = 32;
+constexpr int kBigBucket = 4096;  // largest first-byte bucket bwt_bigbucket_kernel sorts
 // sub-bucket ranks by counting (LDS text): members per load round, and whether
 // every element's state is loaded before the first count
 #ifndef BZ2MI_CNT_UNROLL
@@ -1883,7 +1884,9 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
                                                          uint32_t* __restrict__ orig_out, uint64_t* __restrict__ squeue,
                                                          uint32_t* __restrict__ scount, size_t scap,
                                                          BwtItem* __restrict__ lq, uint32_t* __restrict__ lcount,
-                                                         size_t lcap, uint32_t* __restrict__ present_out) {
+                                                         size_t lcap, uint32_t* __restrict__ present_out,
+                                                         uint64_t* __restrict__ bq, uint32_t* __restrict__ bq_count,
+                                                         size_t bq_cap) {
     __shared__ BwtShared sh;
     __shared__ uint32_t stage[NT * 16], th[256], ts[256];
     const int b = blockIdx.x;
@@ -1918,12 +1921,16 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
     const Sharded<uint64_t> sq{squeue, scount, scap};
     const Sharded<BwtItem> lqs{lq, lcount, lcap};
     const uint32_t nbat = pack_children(sh);
-    const bool large = c > (uint32_t)kSmall;
-    uint32_t nl;
+    // buckets of kSmall < c <= kBigBucket: one workgroup each (bwt_bigbucket_kernel)
+    const bool mid = bq && c > (uint32_t)kSmall && c <= (uint32_t)kBigBucket;
+    const bool large = c > (uint32_t)kSmall && !mid;
+    uint32_t nl, nm;
     const uint32_t rl = wg_excl_sum<NT>(large ? 1u : 0u, sh.tmp, &nl);
+    const uint32_t rm = wg_excl_sum<NT>(mid ? 1u : 0u, sh.tmp, &nm);
     if (t == 0) {
         sh.bcast[0] = nbat ? sq.reserve((uint32_t)b, nbat) : 0u;
         sh.bcast[1] = nl ? lqs.reserve((uint32_t)b, nl) : 0u;
+        if (bq) bq_count[b] = nm;
     }
     __syncthreads();
     if ((uint32_t)t < nbat) {
@@ -1931,6 +1938,135 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
         sq.put((uint32_t)b, sh.bcast[0] + t, sq_pack((uint32_t)b, sh.bat_start[t], bl & 0x7fffffffu, bl >> 31));
     }
     if (large) lqs.put((uint32_t)b, sh.bcast[1] + rl, BwtItem{(uint32_t)b, ex, c, 1});
+    if (mid) bq[(size_t)b * bq_cap + rm] = ((uint64_t)ex << 32) | c;
+}
+
+// ---- kernel 1b (blocks beyond the LDS text): one workgroup per first-byte
+// bucket of kSmall < c <= kBigBucket rotations.  Every rotation's 8 bytes at
+// depth 1 and its BWT byte are gathered once into LDS, counting-sorted by the
+// first of them, and each sub-bucket ranked in LDS (by counting when small, a
+// wave sort otherwise); ties go to the tie list at depth 9.  Replaces the
+// depth-1 partition (a gather, an SA round trip) and the small sorts of its
+// batches (a second gather) for these buckets -- a random 900 KB block's
+// first-byte buckets are ~3,500 rotations.
+struct BigLds {
+    static constexpr bool kKeys = true;
+    uint64_t key[kBigBucket];
+    uint32_t idx[kBigBucket];  // rotation index | BWT byte << 24
+    uint32_t base[257];
+    uint32_t tmp[NW * 2];
+};
+
+__global__ __launch_bounds__(256) void bwt_bigbucket_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+                                                            const uint32_t* __restrict__ lens,
+                                                            uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
+                                                            uint32_t* __restrict__ orig_out,
+                                                            const uint64_t* __restrict__ bq,
+                                                            const uint32_t* __restrict__ bq_count, size_t bq_cap,
+                                                            uint64_t* __restrict__ tl, uint32_t* __restrict__ tcount,
+                                                            size_t tcap, BwtItem* __restrict__ lq,
+                                                            uint32_t* __restrict__ lcount, size_t lcap) {
+    __shared__ BigLds L;
+    const uint32_t b = blockIdx.x;
+    if (blockIdx.y >= bq_count[b]) return;
+    const uint64_t e = bq[(size_t)b * bq_cap + blockIdx.y];
+    const uint32_t start = (uint32_t)(e >> 32), len = (uint32_t)e;
+    const int n = (int)lens[b];
+    const uint8_t* T = blocks + (size_t)b * stride;
+    uint32_t* sa = sa_all + (size_t)b * stride;
+    uint8_t* bw = bwt_out + (size_t)b * stride;
+    uint32_t* orig = orig_out + b;
+    const int t = threadIdx.x;
+    constexpr int PER = kBigBucket / NT;
+    L.base[t] = 0;
+    __syncthreads();
+    uint64_t key[PER];
+    uint32_t ii[PER], slot[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t g = (uint32_t)(j * NT + t);
+        ii[j] = g < len ? sa[start + g] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t g = (uint32_t)(j * NT + t);
+        key[j] = 0;
+        if (g < len) {
+            const uint32_t i = ii[j];
+            key[j] = load8(T, n, i + 1 == (uint32_t)n ? 0u : i + 1);
+            ii[j] = i | ((uint32_t)bwt_byte(T, n, i) << 24);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+        if ((uint32_t)(j * NT + t) < len) slot[j] = atomicAdd(&L.base[key[j] >> 56], 1u);
+    __syncthreads();
+    {
+        uint32_t tot;
+        const uint32_t ex = wg_excl_sum<NT>(L.base[t], L.tmp, &tot);
+        __syncthreads();
+        L.base[t] = ex;
+        if (t == 0) L.base[256] = len;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if ((uint32_t)(j * NT + t) < len) {
+            const uint32_t pos = L.base[key[j] >> 56] + slot[j];
+            L.key[pos] = key[j];
+            L.idx[pos] = ii[j];
+        }
+    }
+    __syncthreads();
+    const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, b, tl + (size_t)b * tcap, tcount + b};
+    // small sub-buckets: ranks by counting
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t p = (uint32_t)(j * NT + t);
+        const bool inseg = p < len;
+        const uint64_t k = inseg ? L.key[p] : 0ull;
+        const uint32_t w = inseg ? L.idx[p] : 0u;
+        const uint32_t c = (uint32_t)(k >> 56);
+        const uint32_t b0 = L.base[c], m = inseg ? L.base[c + 1] - b0 : 0u;
+        const bool mine = inseg && m <= (uint32_t)kSub;
+        const uint32_t i = w & 0xffffffu;
+        uint32_t lt = 0, le = 0, eqlt = 0;
+        for (uint32_t q = 0; q < (mine ? m : 0u); ++q) {
+            const uint64_t kq = L.key[b0 + q];
+            const uint32_t iq = L.idx[b0 + q] & 0xffffffu;
+            lt += kq < k;
+            le += kq <= k;
+            eqlt += (kq == k) & (iq < i);
+        }
+        const uint32_t fin = start + b0 + lt + eqlt;
+        if (mine) {
+            sa[fin] = i;
+            bw[fin] = (uint8_t)(w >> 24);
+            if (i == 0) *orig = fin;
+        }
+        sink.push_agg(mine && le - lt >= 2 && eqlt == 0, Seg{start + b0 + lt, le - lt}, 9);
+    }
+    // larger sub-buckets: a wave sort each (wave w: sub-buckets 64w..64w+63);
+    // beyond kSmall the level queue at depth 2
+    const int lane = lane_id();
+    const uint32_t c = (uint32_t)(wave_id() * 64 + lane);
+    const uint32_t b0 = L.base[c], m = L.base[c + 1] - b0;
+    Scratch s{};
+    s.sa = sa;
+    uint64_t big = __ballot(m > (uint32_t)kSub);
+    while (big) {
+        const int l = __builtin_ctzll(big);
+        big &= big - 1;
+        const uint32_t lb0 = uniform((uint32_t)__shfl((int)b0, l)), lm = uniform((uint32_t)__shfl((int)m, l));
+        if (lm <= (uint32_t)kSmall) {
+            wave_sort_lds_any(T, n, s, start, lb0, lm, 1u, sink, bw, orig, L);
+        } else {
+            for (uint32_t q = (uint32_t)lane; q < lm; q += 64) sa[start + lb0 + q] = L.idx[lb0 + q] & 0xffffffu;
+            if (lane == 0) {
+                const Sharded<BwtItem> lqs{lq, lcount, lcap};
+                lqs.put(b, lqs.reserve(b, 1u), BwtItem{b, start + lb0, lm, 2});
+            }
+        }
+    }
 }
 
 // ---- kernel 1' (blocks of <= kBwtLdsText bytes, replaces kernel 1 and the

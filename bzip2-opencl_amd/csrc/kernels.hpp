@@ -26,7 +26,13 @@ constexpr int kBwtLevels = 4;  // global partition levels (the last one finishes
 __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                                   uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint64_t* squeue,
                                   uint32_t* scount, size_t scap, BwtItem* lq, uint32_t* lcount, size_t lcap,
-                                  uint32_t* present_out);
+                                  uint32_t* present_out, uint64_t* bq, uint32_t* bq_count, size_t bq_cap);
+// buckets of 512 < c <= 4096 rotations listed by bwt_bucket_kernel in bq (per
+// block, bq_cap entries, count bq_count[b]): grid (blocks, 256)
+__global__ void bwt_bigbucket_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
+                                     uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* bq,
+                                     const uint32_t* bq_count, size_t bq_cap, uint64_t* tl, uint32_t* tcount,
+                                     size_t tcap, BwtItem* lq, uint32_t* lcount, size_t lcap);
 // Blocks of <= kBwtLdsText bytes: the first-byte sort and the sort of the
 // small buckets in one launch, the block's text held in LDS (1024 threads, one
 // workgroup per CU).  Large buckets still go to the level queue.
