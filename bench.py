@@ -61,8 +61,10 @@ KSTATS_PROFILE = "profiles/r04_kernel_stats_{data}_v1.csv"
 # the kernels of each timed stage (bz2mi_compress_device, csrc/api.hip)
 STAGE_KERNELS = {
     "front": "fe_summary/runscan/costscan/dmap/chain/resolve (scans + block chain) and fe_rle1_kernel",
-    "bwt": "bwt_block_kernel x2 (mode 0: first-byte scatter + batch sorts; mode 1: blocks the text kernel hands "
-           "back), bwt_text_kernel, bwt_wlevel/level/block_small kernels, bwt_tie_kernel x6, bwt_double_kernel",
+    "bwt": "90 KB blocks: bwt_block_kernel x2 (mode 0: first-byte scatter + batch sorts; mode 1: blocks the text "
+           "kernel hands back), bwt_text_kernel, bwt_wlevel/level/block_small kernels, bwt_tie_kernel x6, "
+           "bwt_double_kernel; 900 KB blocks: bwt_bucket/bigbucket/wlevel/level/small kernels, bwt_tie_kernel x3, "
+           "dbl_* (grid-wide prefix doubling)",
     "mtf": "mtf_kernel<G>",
     "huffman": "huffman_kernel",
     "assemble": "offsets_dev_kernel, assemble_dev_kernel, advance_kernel",
@@ -380,6 +382,12 @@ def main():
     # 900 KB mode (unit 100000, S = 900,000; O_ref900 pins),
     # timed the same way right after the line's own steps
     mode900 = None
+    # one context at a time: each holds its own streams, and two contexts'
+    # streams share the device's hardware queues (GPU_MAX_HW_QUEUES = 4), which
+    # serialises the second context's pipelined stages
+    del out
+    ctx.close()
+    torch.cuda.empty_cache()
     if not args.no_900k and args.unit == 10000 and args.level == 9:
         ctx9 = bz2mi.Context(args.level, args.parallel, 100000, device=local)
         ctx9.stats()
@@ -417,9 +425,6 @@ def main():
     units_n1 = None
     if not args.no_units and world == 1 and args.mode == "compress":
         import copy
-        del out
-        ctx.close()
-        torch.cuda.empty_cache()
         a2 = copy.copy(args)
         a2.units_per_gpu, a2.no_cpu = 4, True
         u = bench_units(a2, 1, emit=False)

@@ -449,11 +449,12 @@ void launch_mtf(int nb, const uint8_t* bwt, size_t stride, const uint32_t* lens,
     // several times over (each wave's tile chain is latency-bound below ~6
     // waves per SIMD), else segments
     // (every instance runs in the tests: 1 GiB batches take G = 1, the 900 KB
-    // mode and small batches 4 / 8; A/B builds: -DBZ2MI_AB_MTF_WAVES=G)
+    // mode (batches of <= ~660 blocks) 16, small batches 4 / 8 / 16; A/B
+    // builds: -DBZ2MI_AB_MTF_WAVES=G)
 #ifdef BZ2MI_AB_MTF_WAVES
     const int g = BZ2MI_AB_MTF_WAVES;
 #else
-    const int g = nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : 8;
+    const int g = nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : nb >= 768 ? 8 : 16;
 #endif
 #define BZ2MI_MTF_LAUNCH(G)                                                                                     \
     hipLaunchKernelGGL(mtf_kernel<G>, dim3(nb), dim3(64 * G), 0, s, bwt, stride, lens, nb, present, mtf_out,      \
@@ -462,7 +463,8 @@ void launch_mtf(int nb, const uint8_t* bwt, size_t stride, const uint32_t* lens,
         case 1: BZ2MI_MTF_LAUNCH(1); break;
         case 2: BZ2MI_MTF_LAUNCH(2); break;
         case 4: BZ2MI_MTF_LAUNCH(4); break;
-        default: BZ2MI_MTF_LAUNCH(8); break;
+        case 8: BZ2MI_MTF_LAUNCH(8); break;
+        default: BZ2MI_MTF_LAUNCH(16); break;
     }
 #undef BZ2MI_MTF_LAUNCH
 }
