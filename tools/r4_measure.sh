@@ -17,7 +17,7 @@ echo "realtext: $(python3 -c "import json; d=json.load(open('$O/bench_realtext.j
 timeout -k 10 300 python3 $R/bench.py --data text --no-cpu --no-units --no-900k $STEPS > $O/bench_text.json 2> $O/bench_text.err || { echo BENCH_TXT_FAILED; tail $O/bench_text.err; exit 1; }
 echo "text: $(python3 -c "import json; d=json.load(open('$O/bench_text.json')); print(d['value'], d['ms_per_step'], d['roofline']['stage_ms'])")"
 fi
-IFS=';' read -ra RS <<< "${RUNS:-random:--data random;realtext:--data realtext;random900k:--data random --unit 100000}"
+IFS=";" read -ra RS <<< "${RUNS:-random:--data random;realtext:--data realtext;text:--data text;random900k:--data random --unit 100000;realtext900k:--data realtext --unit 100000}"
 for spec in "${RS[@]}"; do
   name=${spec%%:*}; args=${spec#*:}
   rm -rf $O/prof_$name
