@@ -1967,9 +1967,11 @@ __global__ __launch_bounds__(256) void bwt_bigbucket_kernel(const uint8_t* __res
                                                             size_t tcap, BwtItem* __restrict__ lq,
                                                             uint32_t* __restrict__ lcount, size_t lcap) {
     __shared__ BigLds L;
-    const uint32_t b = blockIdx.x;
-    if (blockIdx.y >= bq_count[b]) return;
-    const uint64_t e = bq[(size_t)b * bq_cap + blockIdx.y];
+    // grid (256, blocks): consecutive workgroups share a block, so the
+    // concurrent ones gather from a few blocks' text (L2-resident), not all
+    const uint32_t b = blockIdx.y;
+    if (blockIdx.x >= bq_count[b]) return;
+    const uint64_t e = bq[(size_t)b * bq_cap + blockIdx.x];
     const uint32_t start = (uint32_t)(e >> 32), len = (uint32_t)e;
     const int n = (int)lens[b];
     const uint8_t* T = blocks + (size_t)b * stride;
