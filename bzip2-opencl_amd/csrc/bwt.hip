@@ -3235,7 +3235,10 @@ __device__ __forceinline__ void dg_place_by_images(const uint8_t* Tl, int n, uin
 // rank every member by comparing it with the others.  A round that places
 // nothing sends the block back (a group waiting on itself: a tandem repeat).
 // lk: a state per group (0 open, kDgDone, or a link).
-__device__ void text_resolve_all(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa, const uint64_t* dl,
+#ifndef TBK_RES_INL
+#define TBK_RES_INL
+#endif
+__device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa, const uint64_t* dl,
                                  uint32_t ndef, uint64_t* lk, uint8_t* out, uint32_t* orig, TextLds& L) {
     const int t = threadIdx.x, w = wave_id(), lane = lane_id();
     uint32_t* W = L.w[w];
