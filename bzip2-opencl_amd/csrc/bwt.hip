@@ -2973,6 +2973,13 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
 #ifndef TBK_SORT_INL
 #define TBK_SORT_INL __forceinline__
 #endif
+// the batched sort items' SA entries loaded one item ahead (A/B: -DBZ2MI_TEXT_PREFETCH=1;
+// off: its 16 live registers spilled 99 VGPRs of the sort loop, text BWT
+// 31.99 -> 31.64 ms, realtext 74.5 -> 73.6 without it)
+#ifndef BZ2MI_TEXT_PREFETCH
+#define BZ2MI_TEXT_PREFETCH 0
+#endif
+constexpr bool kTextPrefetch = BZ2MI_TEXT_PREFETCH != 0;
 #ifndef TBK_PART_INL
 #define TBK_PART_INL __forceinline__
 #endif
@@ -3737,11 +3744,12 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                 dst[e] = (len <= (uint32_t)kSmall && g < len) ? ld_fresh(sa + st + g) : 0u;
             }
         };
-        if (lo < hi) load(lo, pre);
+        if (kTextPrefetch && lo < hi) load(lo, pre);
         for (uint32_t k = lo; k < hi; ++k) {
             if (uniform(*(volatile uint32_t*)&L.fail)) break;  // the block goes back to the general path
             uint32_t nxt[E];
-            if (k + 1 < hi) load(k + 1, nxt);
+            if (kTextPrefetch && k + 1 < hi) load(k + 1, nxt);
+            if (!kTextPrefetch) load(k, pre);
             const uint64_t it = dl2[k];
             const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
             const uint32_t d = uniform((uint32_t)(it >> 34) & 0xffffu);
@@ -3755,8 +3763,10 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
             TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
 #endif
+            if (kTextPrefetch) {
 #pragma unroll
-            for (int e = 0; e < E; ++e) pre[e] = nxt[e];
+                for (int e = 0; e < E; ++e) pre[e] = nxt[e];
+            }
         }
     }
     __threadfence_block();
