@@ -2880,7 +2880,7 @@ __device__ __forceinline__ int text_cmp_deferred(const uint8_t* Tl, int n, uint3
                                                  uint32_t g, const uint32_t* isa, const uint64_t* dl, uint32_t* link,
                                                  uint32_t* xo);
 
-// Tied items of a wave sort (W[0, tt): index | slot << 17 | group head << 26,// Tied items of a wave sort (W[0, tt): index | slot << 17 | group head << 26,
+// Tied items of a wave sort (W[0, tt): index | slot << 17 | group head << 26,
 // groups in slot order) at depth D: every group of exactly two rotations is
 // ordered by comparing the LDS text directly, 8 bytes at a time, up to
 // kTextPairCap bytes (one lane per pair; the repeats of text tie in pairs),
