@@ -2687,7 +2687,7 @@ constexpr int kTextChain = 32;    // levels a partition goes down with one child
 #endif
 constexpr int kTextTieCap = BZ2MI_TEXT_TIECAP;  // tie depth after which a wave sort defers its tied groups
 #ifndef BZ2MI_TEXT_PAIRCAP
-#define BZ2MI_TEXT_PAIRCAP 64
+#define BZ2MI_TEXT_PAIRCAP 32
 #endif
 constexpr int kTextPairCap = BZ2MI_TEXT_PAIRCAP;  // depth to which two tied rotations are compared directly
 constexpr int kTQ = 512;          // work items per round
@@ -2702,7 +2702,7 @@ constexpr int kPairCap = FW * kTW - FW * 256 - 1;  // the copy steps keep the st
 // copy-processed first-byte buckets (the largest ones); the smaller buckets are
 // sorted whole and copied from in one step
 #ifndef BZ2MI_TEXT_COPYSTEPS
-#define BZ2MI_TEXT_COPYSTEPS 24
+#define BZ2MI_TEXT_COPYSTEPS 12
 #endif
 constexpr int kCopySteps = BZ2MI_TEXT_COPYSTEPS;
 
