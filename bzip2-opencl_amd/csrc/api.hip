@@ -203,7 +203,7 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
                            t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap,
                            t.d_present, c->d_tq[1], tc[1], tcap);
         HIPCHECK(hipGetLastError());
-        hipLaunchKernelGGL(bwt_bigbucket_kernel, dim3(256, nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
+        hipLaunchKernelGGL(bwt_bigbucket_kernel, dim3(256, nb), dim3(kBigBucketThreads), 0, s, t.d_blocks, c->stride, t.d_lens,
                            t.d_sa, t.d_bwt, t.d_orig, c->d_tq[1], tc[1], tcap, c->d_tq[0], tc[0], tcap, c->d_lq[0],
                            lcount + 2 * kBwtShards, lcap);
     }

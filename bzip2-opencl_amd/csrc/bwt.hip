@@ -1954,10 +1954,15 @@ struct BigLds {
     uint64_t key[kBigBucket];
     uint32_t idx[kBigBucket];  // rotation index | BWT byte << 24
     uint32_t base[257];
-    uint32_t tmp[NW * 2];
+    uint32_t tmp[16];
 };
+// threads per big-bucket workgroup (A/B: -DBZ2MI_BIG_NT=256)
+#ifndef BZ2MI_BIG_NT
+#define BZ2MI_BIG_NT 512
+#endif
+constexpr int kBigNT = BZ2MI_BIG_NT;
 
-__global__ __launch_bounds__(256) void bwt_bigbucket_kernel(const uint8_t* __restrict__ blocks, size_t stride,
+__global__ __launch_bounds__(kBigNT) void bwt_bigbucket_kernel(const uint8_t* __restrict__ blocks, size_t stride,
                                                             const uint32_t* __restrict__ lens,
                                                             uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
                                                             uint32_t* __restrict__ orig_out,
@@ -1979,19 +1984,19 @@ __global__ __launch_bounds__(256) void bwt_bigbucket_kernel(const uint8_t* __res
     uint8_t* bw = bwt_out + (size_t)b * stride;
     uint32_t* orig = orig_out + b;
     const int t = threadIdx.x;
-    constexpr int PER = kBigBucket / NT;
-    L.base[t] = 0;
+    constexpr int PER = kBigBucket / kBigNT;
+    if (t < 256) L.base[t] = 0;
     __syncthreads();
     uint64_t key[PER];
     uint32_t ii[PER], slot[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const uint32_t g = (uint32_t)(j * NT + t);
+        const uint32_t g = (uint32_t)(j * kBigNT + t);
         ii[j] = g < len ? sa[start + g] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const uint32_t g = (uint32_t)(j * NT + t);
+        const uint32_t g = (uint32_t)(j * kBigNT + t);
         key[j] = 0;
         if (g < len) {
             const uint32_t i = ii[j];
@@ -2001,19 +2006,19 @@ __global__ __launch_bounds__(256) void bwt_bigbucket_kernel(const uint8_t* __res
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-        if ((uint32_t)(j * NT + t) < len) slot[j] = atomicAdd(&L.base[key[j] >> 56], 1u);
+        if ((uint32_t)(j * kBigNT + t) < len) slot[j] = atomicAdd(&L.base[key[j] >> 56], 1u);
     __syncthreads();
     {
         uint32_t tot;
-        const uint32_t ex = wg_excl_sum<NT>(L.base[t], L.tmp, &tot);
+        const uint32_t ex = wg_excl_sum<kBigNT>(t < 256 ? L.base[t] : 0u, L.tmp, &tot);
         __syncthreads();
-        L.base[t] = ex;
+        if (t < 256) L.base[t] = ex;
         if (t == 0) L.base[256] = len;
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        if ((uint32_t)(j * NT + t) < len) {
+        if ((uint32_t)(j * kBigNT + t) < len) {
             const uint32_t pos = L.base[key[j] >> 56] + slot[j];
             L.key[pos] = key[j];
             L.idx[pos] = ii[j];
@@ -2023,7 +2028,7 @@ __global__ __launch_bounds__(256) void bwt_bigbucket_kernel(const uint8_t* __res
     const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, b, tl + (size_t)b * tcap, tcount + b};
     // small sub-buckets: ranks by counting
     for (int j = 0; j < PER; ++j) {
-        const uint32_t p = (uint32_t)(j * NT + t);
+        const uint32_t p = (uint32_t)(j * kBigNT + t);
         const bool inseg = p < len;
         const uint64_t k = inseg ? L.key[p] : 0ull;
         const uint32_t w = inseg ? L.idx[p] : 0u;
@@ -2050,6 +2055,7 @@ __global__ __launch_bounds__(256) void bwt_bigbucket_kernel(const uint8_t* __res
     // larger sub-buckets: a wave sort each (wave w: sub-buckets 64w..64w+63);
     // beyond kSmall the level queue at depth 2
     const int lane = lane_id();
+    if (wave_id() >= 4) return;  // (waves 0-3 take the 256 sub-buckets)
     const uint32_t c = (uint32_t)(wave_id() * 64 + lane);
     const uint32_t b0 = L.base[c], m = L.base[c + 1] - b0;
     Scratch s{};

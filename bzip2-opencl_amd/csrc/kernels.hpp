@@ -28,7 +28,12 @@ __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const ui
                                   uint32_t* scount, size_t scap, BwtItem* lq, uint32_t* lcount, size_t lcap,
                                   uint32_t* present_out, uint64_t* bq, uint32_t* bq_count, size_t bq_cap);
 // buckets of 512 < c <= 4096 rotations listed by bwt_bucket_kernel in bq (per
-// block, bq_cap entries, count bq_count[b]): grid (256, blocks)
+// block, bq_cap entries, count bq_count[b]): grid (256, blocks) of
+// kBigBucketThreads
+#ifndef BZ2MI_BIG_NT
+#define BZ2MI_BIG_NT 512
+#endif
+constexpr int kBigBucketThreads = BZ2MI_BIG_NT;
 __global__ void bwt_bigbucket_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                      uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* bq,
                                      const uint32_t* bq_count, size_t bq_cap, uint64_t* tl, uint32_t* tcount,
