@@ -57,7 +57,7 @@ def ensure_built():
 
 TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r04_traffic_{data}.json")
 ISSUE_PROFILE = os.path.join(REPO, "profiles", "r04_issue_{data}.json")
-KSTATS_PROFILE = "profiles/r04_kernel_stats_{data}_v2.csv"
+KSTATS_PROFILE = "profiles/r04_kernel_stats_{data}_v3.csv"
 # the kernels of each timed stage (bz2mi_compress_device, csrc/api.hip)
 STAGE_KERNELS = {
     "front": "fe_summary/runscan/costscan/dmap/chain/resolve (scans + block chain) and fe_rle1_kernel",
