@@ -85,6 +85,29 @@ def test_900k_mode_matches_cpuref(bz, cpuref):
         assert bz2.decompress(got) == data
 
 
+@pytest.mark.parametrize("level", [9, 1])
+def test_900k_mode_periodic_and_small_alphabets_match_cpuref(bz, cpuref, level):
+    """Blocks beyond the LDS text (unit 100000) whose tie groups reach the
+    grid-wide doubling's large-group path (periodic blocks: groups of n /
+    period rotations, doubling to h >= n) and its repeat pairs."""
+    from bz2mi import synth
+    rng = np.random.default_rng(0x5EED0905)
+    pattern = rng.integers(0, 256, 3000, dtype=np.uint8).tobytes()
+    cases = {
+        "periodic_ab": b"ab" * (1 << 19),
+        "periodic_sentence": b"the quick brown fox jumps " * 40000,
+        "periodic_3000": pattern * 700,
+        "acgt": synth.small_alphabet_bytes(2 << 20).tobytes(),
+        "zeros": bytes(3 << 20),
+        "mixed": synth.mixed_bytes(4 << 20, segment=512 << 10).tobytes(),
+    }
+    for name, data in cases.items():
+        want = cpuref.compress(data, level, 10, unit=100000, threads=16)
+        got = bz.compress(data, level, 10, unit=100000)
+        assert got == want, (name, level)
+        assert bz2.decompress(got) == data, name
+
+
 def test_small_batches_carry_state(bz, cpuref):
     """Back-end batches of 7 blocks: seed carry-over and bit carry across calls."""
     from bz2mi import synth
