@@ -271,7 +271,10 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         DblGrid G{t.d_blocks, c->stride, t.d_lens, t.d_sa, t.d_bwt, t.d_orig, t.d_groups, t.d_ngroups, t.d_p2list,
                   p2count, c->d_dscratch, dbl_slot_bytes(c->S), c->S, {c->d_dlist[0], c->d_dlist[1]},
                   {c->d_dlarge[0], c->d_dlarge[1]}, c->d_dctr};
-        const dim3 grid((unsigned)c->cus * 8), blk256(256);
+#ifndef BZ2MI_AB_DBL_GRID
+#define BZ2MI_AB_DBL_GRID 4
+#endif
+        const dim3 grid((unsigned)c->cus * BZ2MI_AB_DBL_GRID), blk256(256);
         HIPCHECK(hipMemsetAsync(c->d_dctr, 0, sizeof(uint32_t) * kDblCtr * (kDblMaxRounds + 2), s));
         hipLaunchKernelGGL(dbl_init_rank_kernel, grid, blk256, 0, s, G);
         hipLaunchKernelGGL(dbl_init_groups_kernel, grid, blk256, 0, s, G);
