@@ -775,9 +775,12 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     // scatter); after it one batch and batches of 3072 both give 26.0 -- one
     // batch keeps the per-stage event times per launch (the roofline figures).
     c->batch_blocks = std::min(16384, std::max(64, (int)((1536u << 20) / (unsigned)c->S)));
-    if (c->S > bz2mi::kBwtLdsText) {  // the grid doubling's scratch: about 24 GB per batch at most
+    // the grid doubling's scratch: at most ~52 GB per batch, so a 1 GiB input
+    // is one batch at S = 900,000 (1,193 blocks; measured one batch 35.1 GB/s
+    // vs two of 666 blocks 33.6), allocated as the batches grow
+    if (c->S > bz2mi::kBwtLdsText) {
         const size_t per = bz2mi::dbl_slot_bytes(c->S) + 16 * (bz2mi::dbl_list_cap(c->S) + bz2mi::dbl_large_cap(c->S));
-        c->batch_blocks = std::min(c->batch_blocks, std::max(64, (int)((size_t)24e9 / per)));
+        c->batch_blocks = std::min(c->batch_blocks, std::max(64, (int)((size_t)52e9 / per)));
     }
     if (const char* e = getenv("BZ2MI_BATCH_BLOCKS")) c->batch_blocks = std::max(1, atoi(e));
     for (auto& e : c->ev) (void)hipEventCreate(&e);
