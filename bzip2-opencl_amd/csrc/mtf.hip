@@ -448,13 +448,13 @@ void launch_mtf(int nb, const uint8_t* bwt, size_t stride, const uint32_t* lens,
     // waves per block: one while the blocks alone fill the chip's SIMDs
     // several times over (each wave's tile chain is latency-bound below ~6
     // waves per SIMD), else segments
-    // (every instance runs in the tests: 1 GiB batches take G = 1, the 900 KB
-    // mode (batches of <= ~660 blocks) 16, small batches 4 / 8 / 16; A/B
-    // builds: -DBZ2MI_AB_MTF_WAVES=G)
+    // (1 GiB batches take G = 1, the 900 KB mode (1,193 blocks per GiB) 16 --
+    // measured 5.95 vs 6.43 ms for G = 8 --, small batches 4 / 16; G = 8 only
+    // in A/B builds: -DBZ2MI_AB_MTF_WAVES=G)
 #ifdef BZ2MI_AB_MTF_WAVES
     const int g = BZ2MI_AB_MTF_WAVES;
 #else
-    const int g = nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : nb >= 768 ? 8 : 16;
+    const int g = nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : 16;
 #endif
 #define BZ2MI_MTF_LAUNCH(G)                                                                                     \
     hipLaunchKernelGGL(mtf_kernel<G>, dim3(nb), dim3(64 * G), 0, s, bwt, stride, lens, nb, present, mtf_out,      \
