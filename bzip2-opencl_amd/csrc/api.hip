@@ -107,45 +107,70 @@ int stage_front(bz2mi_ctx* c, Batch& t, const FrontBufs& f, const uint8_t* d_x, 
     return BZ2MI_OK;
 }
 
+// Blocks whose text fits in LDS take the block kernels; the rest take the
+// grid path (big buckets, grid-wide doubling).  One predicate for the path and
+// for the scratch it needs (A/B builds with -DBZ2MI_AB_NO_LDSTEXT send every
+// block size to the grid path).
+bool lds_text_path(int S) {
+#ifdef BZ2MI_AB_NO_LDSTEXT
+    (void)S;
+    return false;
+#else
+    return S <= bz2mi::kBwtLdsText;
+#endif
+}
+
+// The BWT's queues and (grid path) doubling scratch for batches of up to nb
+// blocks; shared by the batches, so BWTs run one at a time (stream sA).
+void free_bwt_scratch(bz2mi_ctx* c) {
+    for (void* p : {(void*)c->d_sq, (void*)c->d_lq[0], (void*)c->d_lq[1], (void*)c->d_tq[0], (void*)c->d_tq[1],
+                    (void*)c->d_tc, (void*)c->d_lspill, (void*)c->d_scb, (void*)c->d_dscratch, (void*)c->d_dlist[0],
+                    (void*)c->d_dlist[1], (void*)c->d_dlarge[0], (void*)c->d_dlarge[1], (void*)c->d_dctr})
+        if (p) (void)hipFree(p);
+    c->d_dscratch = nullptr;
+    c->d_dlist[0] = c->d_dlist[1] = c->d_dlarge[0] = c->d_dlarge[1] = nullptr;
+    c->d_dctr = nullptr;
+    c->d_sq = nullptr;
+    c->d_lq[0] = c->d_lq[1] = nullptr;
+    c->d_tq[0] = c->d_tq[1] = nullptr;
+    c->d_tc = nullptr;
+    c->d_lspill = nullptr;
+    c->d_scb = nullptr;
+    c->bwtq_blocks = 0;
+}
+
+int ensure_bwt_scratch(bz2mi_ctx* c, int nb) {
+    using namespace bz2mi;
+    if (nb <= c->bwtq_blocks) return BZ2MI_OK;
+    free_bwt_scratch(c);
+    const size_t B = (size_t)std::max(nb, 16);
+    const size_t Bs = (B + kBwtShards - 1) / kBwtShards;  // blocks per shard
+    int r;
+    if ((r = dalloc(&c->d_sq, kBwtShards * Bs * bwt_squeue_per_block(c->S)))) return r;
+    if ((r = dalloc(&c->d_lq[0], kBwtShards * Bs * bwt_lqueue_per_block(c->S)))) return r;
+    if ((r = dalloc(&c->d_lq[1], kBwtShards * Bs * bwt_lqueue_per_block(c->S)))) return r;
+    if ((r = dalloc(&c->d_tq[0], B * bwt_squeue_per_block(c->S)))) return r;
+    if ((r = dalloc(&c->d_tq[1], B * bwt_squeue_per_block(c->S)))) return r;
+    if ((r = dalloc(&c->d_tc, 2 * B))) return r;
+    if ((r = dalloc(&c->d_lspill, B * c->stride))) return r;
+    if ((r = dalloc(&c->d_scb, B))) return r;
+    if (!lds_text_path(c->S)) {
+        if ((r = dalloc(&c->d_dscratch, B * dbl_slot_bytes(c->S)))) return r;
+        for (int k = 0; k < 2; ++k) {
+            if ((r = dalloc(&c->d_dlist[k], B * dbl_list_cap(c->S)))) return r;
+            if ((r = dalloc(&c->d_dlarge[k], B * dbl_large_cap(c->S)))) return r;
+        }
+        if ((r = dalloc(&c->d_dctr, (size_t)kDblCtr * (kDblMaxRounds + 2)))) return r;
+    }
+    c->bwtq_blocks = (int)B;
+    return BZ2MI_OK;
+}
+
 int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     using namespace bz2mi;
-    if (nb > c->bwtq_blocks) {  // queues are shared by the batches: BWTs run one at a time
+    if (nb > c->bwtq_blocks) {  // the queues are reallocated: earlier BWTs on s must be done
         HIPCHECK(hipStreamSynchronize(s));
-        for (void* p : {(void*)c->d_sq, (void*)c->d_lq[0], (void*)c->d_lq[1], (void*)c->d_tq[0], (void*)c->d_tq[1],
-                        (void*)c->d_tc, (void*)c->d_lspill, (void*)c->d_scb, (void*)c->d_dscratch,
-                        (void*)c->d_dlist[0], (void*)c->d_dlist[1], (void*)c->d_dlarge[0], (void*)c->d_dlarge[1],
-                        (void*)c->d_dctr})
-            if (p) (void)hipFree(p);
-        c->d_dscratch = nullptr;
-        c->d_dlist[0] = c->d_dlist[1] = c->d_dlarge[0] = c->d_dlarge[1] = nullptr;
-        c->d_dctr = nullptr;
-        c->d_sq = nullptr;
-        c->d_lq[0] = c->d_lq[1] = nullptr;
-        c->d_tq[0] = c->d_tq[1] = nullptr;
-        c->d_tc = nullptr;
-        c->d_lspill = nullptr;
-        c->d_scb = nullptr;
-        c->bwtq_blocks = 0;
-        const size_t B = (size_t)std::max(nb, 16);
-        const size_t Bs = (B + kBwtShards - 1) / kBwtShards;  // blocks per shard
-        int r;
-        if ((r = dalloc(&c->d_sq, kBwtShards * Bs * bwt_squeue_per_block(c->S)))) return r;
-        if ((r = dalloc(&c->d_lq[0], kBwtShards * Bs * bwt_lqueue_per_block(c->S)))) return r;
-        if ((r = dalloc(&c->d_lq[1], kBwtShards * Bs * bwt_lqueue_per_block(c->S)))) return r;
-        if ((r = dalloc(&c->d_tq[0], B * bwt_squeue_per_block(c->S)))) return r;
-        if ((r = dalloc(&c->d_tq[1], B * bwt_squeue_per_block(c->S)))) return r;
-        if ((r = dalloc(&c->d_tc, 2 * B))) return r;
-        if ((r = dalloc(&c->d_lspill, B * c->stride))) return r;
-        if ((r = dalloc(&c->d_scb, B))) return r;
-        if (c->S > kBwtLdsText) {
-            if ((r = dalloc(&c->d_dscratch, B * dbl_slot_bytes(c->S)))) return r;
-            for (int k = 0; k < 2; ++k) {
-                if ((r = dalloc(&c->d_dlist[k], B * dbl_list_cap(c->S)))) return r;
-                if ((r = dalloc(&c->d_dlarge[k], B * dbl_large_cap(c->S)))) return r;
-            }
-            if ((r = dalloc(&c->d_dctr, (size_t)kDblCtr * (kDblMaxRounds + 2)))) return r;
-        }
-        c->bwtq_blocks = (int)B;
+        if (int r = ensure_bwt_scratch(c, nb)) return r;
     }
     const size_t Bs = ((size_t)c->bwtq_blocks + kBwtShards - 1) / kBwtShards;
     const size_t scap = Bs * bwt_squeue_per_block(c->S), lcap = Bs * bwt_lqueue_per_block(c->S);
@@ -161,14 +186,9 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     uint32_t* pull = t.d_bcnt + 769;
     // A/B builds only (-DBZ2MI_AB_NO_LDSTEXT / _NO_TEXTBWT / _NO_WLEVEL): the
     // product has no run-time path switches
-#ifdef BZ2MI_AB_NO_LDSTEXT
-    constexpr bool lds_text = false;
-#else
-    constexpr bool lds_text = true;
-#endif
     // LDS-text path (blocks fit in LDS): the small batches of the levels go to
     // per-block lists (counts d_scb, capacity tcap each) instead of the shards
-    const bool blk = lds_text && c->S <= kBwtLdsText;
+    const bool blk = lds_text_path(c->S);
     uint32_t* sq_count = blk ? c->d_scb : scount;
     const size_t sq_cap = blk ? tcap : scap;
     const uint32_t smask = blk ? 0xffffffffu : (uint32_t)(kBwtShards - 1);
@@ -198,7 +218,10 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
         }
     } else {
         // mid-size first-byte buckets listed in the second tie list (free
-        // until the tie rounds), sorted whole by bwt_bigbucket_kernel
+        // until the tie rounds), sorted whole by bwt_bigbucket_kernel; its
+        // counts start at zero (the bucket kernel also writes them, 0/1-byte
+        // blocks included)
+        HIPCHECK(hipMemsetAsync(tc[1], 0, nb * sizeof(uint32_t), s));
         hipLaunchKernelGGL(bwt_bucket_kernel, dim3(nb), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, nb, t.d_sa,
                            t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap,
                            t.d_present, c->d_tq[1], tc[1], tcap);
@@ -554,12 +577,29 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
         if ((r = run_chain(c, c->fe, d_x, n, n, 0, true, &nb, nullptr, s))) return r;
     }
     HIPCHECK(hipEventRecord(c->ev[7], s));
-    // batches
-    const uint64_t bsz = (uint64_t)c->batch_blocks;
+    // batches: the batch buffers and the BWT scratch are sized before the
+    // pipeline starts; when an allocation fails (another context or process
+    // holds much of HBM) every batch buffer is freed and the batch halved
+    uint64_t bsz = (uint64_t)c->batch_blocks;
+    for (;;) {
+        const uint64_t want = std::max<uint64_t>(std::min(bsz, nb), 1);
+        const int sets_try = (int)std::min<uint64_t>(nb ? (nb + bsz - 1) / bsz : 1, kSets);
+        r = BZ2MI_OK;
+        for (int k = 0; k < sets_try && !r; ++k) r = ensure_batch(c, c->sets[k], (int)want);
+        if (!r && (int)want > c->bwtq_blocks) {
+            HIPCHECK(hipStreamSynchronize(c->sA));
+            r = ensure_bwt_scratch(c, (int)want);
+        }
+        if (!r) break;
+        if (want <= 1) return r;
+        for (hipStream_t st : {c->sA, c->sM, c->sB}) HIPCHECK(hipStreamSynchronize(st));
+        for (Batch& t : c->sets) free_batch(t);
+        free_bwt_scratch(c);
+        (void)hipGetLastError();
+        bsz = (want + 1) / 2;
+        c->batch_blocks = (int)bsz;
+    }
     const uint64_t nbat = nb ? (nb + bsz - 1) / bsz : 1;
-    const int sets_used = (int)std::min<uint64_t>(nbat, kSets);
-    for (int k = 0; k < sets_used; ++k)
-        if ((r = ensure_batch(c, c->sets[k], (int)std::max<uint64_t>(std::min(bsz, nb), 1)))) return r;
     // output: word-aligned destination, else an aligned staging buffer
     uint32_t* out32 = (uint32_t*)d_out;
     const bool staged = ((uintptr_t)d_out & 3) != 0;
@@ -754,7 +794,7 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
             occ = 4;
         c->wlevel_grid = std::max(8, cus * occ / 8 * 8);
     }
-    if ((c->S <= bz2mi::kBwtLdsText && dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S))) ||
+    if ((bz2mi::host::lds_text_path(c->S) && dalloc(&c->d_scratch, c->bwt_slots * bz2mi::bwt_slot_bytes(c->S))) ||
         dalloc(&c->d_lscratch, c->level_slots * bz2mi::bwt_level_slot_bytes(c->S)) ||
         dalloc(&c->d_state, (size_t)c->p * bz2mi::kMaxAlpha) || dalloc(&c->d_sd, 1) || dalloc(&c->d_vol, 4)) {
         bz2mi_destroy(c);
@@ -778,9 +818,14 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     // the grid doubling's scratch: at most ~52 GB per batch, so a 1 GiB input
     // is one batch at S = 900,000 (1,193 blocks; measured one batch 35.1 GB/s
     // vs two of 666 blocks 33.6), allocated as the batches grow
-    if (c->S > bz2mi::kBwtLdsText) {
+    // -- and at most half of the HBM free when the context is made (a second
+    // context or process on the GPU); compress_device_impl halves the batch
+    // further if an allocation still fails
+    if (!bz2mi::host::lds_text_path(c->S)) {
         const size_t per = bz2mi::dbl_slot_bytes(c->S) + 16 * (bz2mi::dbl_list_cap(c->S) + bz2mi::dbl_large_cap(c->S));
-        c->batch_blocks = std::min(c->batch_blocks, std::max(64, (int)((size_t)52e9 / per)));
+        size_t budget = (size_t)52e9, fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) budget = std::min(budget, fr / 2);
+        c->batch_blocks = std::min(c->batch_blocks, std::max(16, (int)(budget / per)));
     }
     if (const char* e = getenv("BZ2MI_BATCH_BLOCKS")) c->batch_blocks = std::max(1, atoi(e));
     for (auto& e : c->ev) (void)hipEventCreate(&e);
@@ -907,12 +952,31 @@ int bz2mi_finish(bz2mi_ctx* c, uint8_t* out, size_t cap, size_t* out_len) {
 namespace {
 constexpr size_t kPinBytes = (size_t)16 << 20;
 
-int ensure_pinned(bz2mi_ctx* c) {
-    if (c->h_pin[0]) return BZ2MI_OK;
+void free_pinned(bz2mi_ctx* c) {
     for (int k = 0; k < 2; ++k) {
-        if (hipHostMalloc((void**)&c->h_pin[k], kPinBytes, hipHostMallocDefault) != hipSuccess)
+        if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
+        if (c->ev_pin[k]) (void)hipEventDestroy(c->ev_pin[k]);
+        c->h_pin[k] = nullptr;
+        c->ev_pin[k] = nullptr;
+    }
+}
+
+// all four (two buffers, two events) or none: a partial failure frees what
+// was made, so the next call retries instead of using a null buffer/event
+int ensure_pinned(bz2mi_ctx* c) {
+    if (c->h_pin[0] && c->h_pin[1] && c->ev_pin[0] && c->ev_pin[1]) return BZ2MI_OK;
+    free_pinned(c);
+    for (int k = 0; k < 2; ++k) {
+        if (hipHostMalloc((void**)&c->h_pin[k], kPinBytes, hipHostMallocDefault) != hipSuccess) {
+            c->h_pin[k] = nullptr;
+            free_pinned(c);
             return fail(BZ2MI_EDEVICE, "hipHostMalloc failed");
-        HIPCHECK(hipEventCreateWithFlags(&c->ev_pin[k], hipEventDisableTiming));
+        }
+        if (hipEventCreateWithFlags(&c->ev_pin[k], hipEventDisableTiming) != hipSuccess) {
+            c->ev_pin[k] = nullptr;
+            free_pinned(c);
+            return fail(BZ2MI_EDEVICE, "hipEventCreate failed");
+        }
     }
     return BZ2MI_OK;
 }

@@ -1899,6 +1899,7 @@ __global__ __launch_bounds__(256) void bwt_bucket_kernel(const uint8_t* __restri
         if (t == 0) {
             if (n == 1) out[0] = T[0];
             orig_out[b] = 0;
+            if (bq) bq_count[b] = 0;  // no mid-size buckets: the big-bucket kernel sees an empty list
         }
         if (t < 8) present_out[(size_t)b * 8 + t] = (n == 1 && (T[0] >> 5) == t) ? 1u << (T[0] & 31) : 0u;
         return;
@@ -2722,7 +2723,7 @@ struct TextLds {
     uint32_t cstart[257];             // first-byte bucket starts
     uint32_t tmp[FW];
     uint32_t wlo[FW], whi[FW];        // a wave's range of pair entries (the deal)
-    uint32_t qn[2], fail, nflag, ndef, nitems;
+    uint32_t qn[2], fail, nflag, ndef, nitems, next_item;
     uint8_t order[256];               // bytes by ascending bucket size
     uint8_t rank[256];                // position of a byte in that order
     uint8_t target[256];
@@ -2984,6 +2985,11 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
 // 31.99 -> 31.64 ms, realtext 74.5 -> 73.6 without it)
 #ifndef BZ2MI_TEXT_PREFETCH
 #define BZ2MI_TEXT_PREFETCH 0
+#endif
+// A/B: round-0 sort items pulled by the waves from an LDS counter instead of
+// the static deal
+#ifndef BZ2MI_TEXT_DYNDEAL
+#define BZ2MI_TEXT_DYNDEAL 0
 #endif
 constexpr bool kTextPrefetch = BZ2MI_TEXT_PREFETCH != 0;
 #ifndef TBK_PART_INL
@@ -3260,7 +3266,8 @@ __device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t*
     __syncthreads();
     uint32_t before = 0xffffffffu;
     bool forced = false;  // the previous round ordered the open roots by plain comparison
-    for (;;) {
+    for (uint32_t rr = 0;; ++rr) {
+        TBK_T(12, rr << 12 | min(ndef, 4095u));
 #ifdef BZ2MI_PHASES
         if (t == 0) atomicAdd(&g_tbk_res[3], 1ull);
 #endif
@@ -3324,6 +3331,7 @@ __device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t*
         __syncthreads();
         // (2) links
         for (int jump = 0; jump < 32; ++jump) {
+            TBK_T(13, rr << 8 | (uint32_t)jump);
 #ifdef BZ2MI_PHASES
             if (t == 0) atomicAdd(&g_tbk_res[4], 1ull);
 #endif
@@ -3443,6 +3451,7 @@ __device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t*
         __syncthreads();
         const uint32_t left = uniform(L.qn[0]);
         if (left == 0 || uniform(L.fail)) break;
+        TBK_T(14, rr << 12 | min(left, 4095u));
         if (left >= before && !forced) {
             // no group placed this round: the open groups that are not
             // linked (the roots the linked ones wait on) are ordered by plain
@@ -3717,6 +3726,33 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     __threadfence_block();
     __syncthreads();
     const uint32_t nitems = uniform(L.nitems);
+#if BZ2MI_TEXT_DYNDEAL
+    // A/B: every wave pulls its next item from an LDS counter
+    if (t == 0) L.next_item = 0;
+    __syncthreads();
+    for (uint32_t guard = 0;; ++guard) {
+        uint32_t kk = 0;
+        if (lane == 0) kk = atomicAdd(&L.next_item, 1u);
+        const uint32_t k = uniform(kk);
+        if (k >= nitems || guard > nitems) break;
+        if (uniform(*(volatile uint32_t*)&L.fail)) break;
+        constexpr int E = kSmall / 64;
+        uint32_t pre[E];
+        const uint64_t it = dl2[k];
+        const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
+        const uint32_t d = uniform((uint32_t)(it >> 34) & 0xffffu);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t g = (uint32_t)(e * 64 + lane);
+            pre[e] = (seg.len <= (uint32_t)kSmall && g < seg.len) ? ld_fresh(sa + seg.start + g) : 0u;
+        }
+        TBK_T(2, seg.len);
+        if (seg.len <= (uint32_t)kSmall) text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
+        else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, 0);
+        TBK_T(10, k);
+    }
+    if (false)
+#endif
     {
         // deal the items in equal shares of work (contiguous ranges of the list)
         const uint32_t per = (nitems + FT - 1) / FT;
@@ -3735,6 +3771,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     }
     __threadfence_block();
     __syncthreads();
+#if BZ2MI_TEXT_DYNDEAL
+    if (false)
+#endif
     {
         // this wave's items, the next one's SA entries loaded while the
         // current one is sorted

@@ -193,6 +193,9 @@ int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks);
 void free_batch(Batch& t);
 int stage_front(bz2mi_ctx* c, Batch& t, const FrontBufs& f, const uint8_t* d_x, size_t n, uint64_t first,
                 uint64_t cnt, hipStream_t s);
+bool lds_text_path(int S);
+int ensure_bwt_scratch(bz2mi_ctx* c, int nb);
+void free_bwt_scratch(bz2mi_ctx* c);
 int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s);
 int stage_mtf(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s);
 int stage_seed(bz2mi_ctx* c, Batch& t, int nb, uint64_t first_block, uint32_t* state, hipStream_t s);

@@ -238,3 +238,87 @@ def test_outputstream_mirror_matches_cpuref(bz, cpuref, tmp_path):
         r = subprocess.run(args, capture_output=True)
         assert r.returncode == 0, r.stderr
         assert outp.read_bytes() == cpuref.compress(data, level, p, threads=16)
+
+
+def _no_runs(n: int, seed: int) -> bytes:
+    """Random bytes with no two neighbours equal: no RLE1 runs, so the raw
+    bytes are the RLE1 bytes and block boundaries are easy to place."""
+    rng = np.random.default_rng(seed)
+    d = rng.integers(1, 256, n, dtype=np.int64)
+    return (np.cumsum(d) % 256).astype(np.uint8).tobytes()
+
+
+@pytest.mark.parametrize("level", [9, 1])
+def test_900k_mode_tiny_blocks_match_cpuref(bz, cpuref, level):
+    """Blocks of 0/1 bytes in the 900 KB mode (the big-bucket count
+    of a 1-byte block was left unwritten): a 1-byte stream, a 2-byte stream, and
+    a stream whose last block is exactly 1 byte, in one batch with many full
+    blocks and on their own -- equal to cpu_ref and decoding back."""
+    S = level * 100000
+    base = _no_runs(3 * S, 0x5EED0906)
+    blocks, _ = cpuref.split(base, S)
+    n0 = len(blocks[0])
+    tail1 = base[: n0 + 1]
+    assert [len(b) for b in cpuref.split(tail1, S)[0]] == [n0, 1]
+    tail1_many = base[: 2 * n0 + 1]
+    assert [len(b) for b in cpuref.split(tail1_many, S)[0]] == [n0, n0, 1]
+    for name, data in {"one": b"x", "two": b"xy", "tail1": tail1, "tail1_many": tail1_many}.items():
+        for p in (10, 1):
+            got = bz.compress(data, level, p, unit=100000)
+            assert got == cpuref.compress(data, level, p, unit=100000, threads=16), (name, p)
+            assert bz2.decompress(got) == data, name
+    # a context reused after a wide block: a 1-byte block must not see its predecessor's lists
+    ctx = bz.Context(level, 10, 100000)
+    for data in (base, b"z", tail1, b"q"):
+        assert ctx.compress(data) == cpuref.compress(data, level, 10, unit=100000, threads=16)
+
+
+@pytest.mark.timeout(600)
+def test_900k_mode_random_1gib_matches_cpuref(bz, cpuref):
+    """The bench's mode_900k workload at its own size: 1 GiB of random bytes
+    (the C2 seed) at -9 in the 900 KB mode, one batch of 1,194 blocks through
+    the big-bucket kernel and the grid doubling -- the C restatement's stream
+    byte for byte, decoding back on the device."""
+    import torch
+    n = 1 << 30
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0001)
+    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    cap = bz.compress_bound(n, 9, 100000)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    ctx = bz.Context(9, 10, 100000)
+    m = ctx.compress_device(x.data_ptr(), n, out.data_ptr(), cap)
+    stream = out[:m].cpu().numpy().tobytes()
+    host = x.cpu().numpy().tobytes()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    assert stream == cpuref.compress(host, 9, 10, unit=100000, threads=threads)
+    y = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d = bz.Decompressor(100000)
+    assert d.decompress_device(out.data_ptr(), m, y.data_ptr(), n) == n
+    assert torch.equal(x, y)
+
+
+def test_900k_mode_under_memory_pressure(bz, cpuref):
+    """Most of HBM held by another allocation (all but 8 GiB): the 900 KB mode
+    sizes its batches from the free memory (several batches), and a batch
+    that still does not fit (forced with a batch far above what is left) is
+    halved until it does; the stream stays the C restatement's."""
+    import torch
+    from bz2mi import synth
+    free, _total = torch.cuda.mem_get_info()
+    hold = torch.empty(max(0, free - (8 << 30)), dtype=torch.uint8, device="cuda")
+    try:
+        data = synth.random_bytes(256 << 20).tobytes()
+        want = cpuref.compress(data, 9, 10, unit=100000, threads=16)
+        assert bz.compress(data, 9, 10, unit=100000) == want
+        os.environ["BZ2MI_BATCH_BLOCKS"] = "100000"
+        try:
+            got = bz.compress(data, 9, 10, unit=100000)
+        finally:
+            del os.environ["BZ2MI_BATCH_BLOCKS"]
+        assert got == want
+        text = synth.realtext_bytes(24 << 20).tobytes()
+        assert bz.compress(text, 9, 10, unit=100000) == cpuref.compress(text, 9, 10, unit=100000, threads=16)
+    finally:
+        del hold
+        torch.cuda.empty_cache()
