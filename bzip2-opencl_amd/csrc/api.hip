@@ -166,6 +166,22 @@ int ensure_bwt_scratch(bz2mi_ctx* c, int nb) {
     return BZ2MI_OK;
 }
 
+// Device bytes per block of one batch set (ensure_batch) and of the BWT
+// scratch (ensure_bwt_scratch): what a batch of B blocks costs, for sizing
+// batches against the free HBM.
+size_t batch_block_bytes(const bz2mi_ctx* c) {
+    const size_t st = c->stride;
+    return 2 * st + 4 * st + 8 * bz2mi::bwt_group_stride(st) + 2 * c->mtf_stride + 4 * c->payload_words +
+           8 * (size_t)bz2mi::kMaxAlpha + 32 + 64;
+}
+size_t bwt_block_bytes(const bz2mi_ctx* c) {
+    using namespace bz2mi;
+    size_t b = 3 * 8 * bwt_squeue_per_block(c->S) + 2 * sizeof(BwtItem) * bwt_lqueue_per_block(c->S) + 4 * c->stride +
+               16;
+    if (!lds_text_path(c->S)) b += dbl_slot_bytes(c->S) + 16 * (dbl_list_cap(c->S) + dbl_large_cap(c->S));
+    return b;
+}
+
 int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     using namespace bz2mi;
     if (nb > c->bwtq_blocks) {  // the queues are reallocated: earlier BWTs on s must be done
@@ -256,7 +272,7 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
             continue;
         }
         hipLaunchKernelGGL(bwt_level_kernel, dim3(c->level_slots), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens,
-                           t.d_sa, t.d_bwt, t.d_orig, c->d_lscratch, bwt_level_slot_bytes(c->S), c->S, c->d_lq[d & 1],
+                           t.d_sa, t.d_bwt, t.d_orig, c->d_lscratch, c->d_lspill, bwt_level_slot_bytes(c->S), c->S, c->d_lq[d & 1],
                            lcount + d * kBwtShards, c->d_lq[(d + 1) & 1], lcount + (d + 1) * kBwtShards, lcap,
                            c->d_sq, sq_count, sq_cap, t.d_groups, t.d_ngroups, t.d_p2list, p2count,
                            d == kBwtLevels ? 1 : 0, smask);
@@ -581,6 +597,24 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
     // pipeline starts; when an allocation fails (another context or process
     // holds much of HBM) every batch buffer is freed and the batch halved
     uint64_t bsz = (uint64_t)c->batch_blocks;
+    {
+        // at most ~80 % of what is free now, counting the buffers this context
+        // already holds (they are reused or freed below)
+        size_t fr = 0, tot = 0;
+        if (nb && hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            size_t held = (size_t)c->bwtq_blocks * bwt_block_bytes(c);
+            for (const Batch& t : c->sets) held += (size_t)t.cap * batch_block_bytes(c);
+            const size_t avail = (fr + held) / 10 * 8;
+            const uint64_t want = std::min(bsz, nb);
+            const size_t per1 = batch_block_bytes(c) + bwt_block_bytes(c);  // one batch: one set
+            const size_t per3 = kSets * batch_block_bytes(c) + bwt_block_bytes(c);
+            if (want * (want < nb ? per3 : per1) > avail) {
+                const uint64_t fit = std::max<uint64_t>(1, avail / per3);
+                const uint64_t k = (nb + fit - 1) / fit;  // batches
+                bsz = std::max<uint64_t>(1, (nb + k - 1) / k);
+            }
+        }
+    }
     for (;;) {
         const uint64_t want = std::max<uint64_t>(std::min(bsz, nb), 1);
         const int sets_try = (int)std::min<uint64_t>(nb ? (nb + bsz - 1) / bsz : 1, kSets);

@@ -1064,6 +1064,16 @@ __device__ __forceinline__ uint32_t lds_tie_round_any(const uint8_t* T, int n, S
     return lds_tie_round<8>(T, n, s, base, t, D, bwt, orig, idx);
 }
 
+// the same for at most 64 * MAXE items (no instance of the larger rounds)
+template <int MAXE>
+__device__ __forceinline__ uint32_t lds_tie_round_upto(const uint8_t* T, int n, Scratch& s, uint32_t base, uint32_t t,
+                                                       uint32_t D, uint8_t* bwt, uint32_t* orig, uint32_t* idx) {
+    if (t <= 64) return lds_tie_round<1>(T, n, s, base, t, D, bwt, orig, idx);
+    if (MAXE <= 2 || t <= 128) return lds_tie_round<MAXE <= 2 ? MAXE : 2>(T, n, s, base, t, D, bwt, orig, idx);
+    if (MAXE <= 4 || t <= 256) return lds_tie_round<MAXE <= 4 ? MAXE : 4>(T, n, s, base, t, D, bwt, orig, idx);
+    return lds_tie_round<MAXE>(T, n, s, base, t, D, bwt, orig, idx);
+}
+
 // groups still tied at the depth limit: SA entries written, groups to the sink
 __device__ __forceinline__ void lds_tie_spill(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t base,
                                            uint32_t t, uint32_t D, const GroupSink& sink,
@@ -1119,12 +1129,13 @@ __device__ __forceinline__ uint32_t wave_sort_lds_text(const uint8_t* __restrict
 // sorted into LDS sub-buckets first and its keys are gathered from the text
 // once.  (Any placement of unsorted items over the slots is a valid input of
 // the bitonic network.)
-template <int ES>
+template <int ES, int PE>
 __device__ __forceinline__ uint32_t wave_sort_pre_text(const uint8_t* __restrict__ T, int n, Scratch& s,
                                                        uint32_t start, uint32_t m, uint32_t d,
                                                        uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
                                                        uint32_t* __restrict__ idx,
-                                                       const uint32_t (&pre)[kSmall / 64]) {
+                                                       const uint32_t (&pre)[PE]) {
+    static_assert(ES <= PE, "slots");
     const int lane = lane_id();
     uint64_t key[ES];
 #pragma unroll
@@ -1496,11 +1507,14 @@ __device__ __forceinline__ size_t shard_locate(const ShardIndex& si, uint32_t q,
 // (singletons are final).  Wave 0 packs with wave scans (4 children per
 // lane); returns the batch count (sh.bat_*).
 // One wave packs `hist`; w0 / w1 are 256-word scratch; returns the batch count.
+template <int SMALL = kSmall>
 __device__ __forceinline__ uint32_t pack_children_wave(const uint32_t* hist, uint32_t* w0, uint32_t* w1,
                                                        uint32_t* bat_start, uint32_t* bat_len) {
     {
         const int lane = lane_id();
-        constexpr uint32_t kHalf = kSmall / 2;
+        constexpr uint32_t kHalf = SMALL / 2;
+        constexpr int kWin = SMALL == 512 ? 8 : 7;  // log2(kHalf): batch windows
+        static_assert((1u << kWin) == kHalf, "window");
         uint32_t m[4], pos[4], sinc[4], brk[4];
         uint32_t tot = 0, stot = 0, btot = 0;
 #pragma unroll
@@ -1533,14 +1547,14 @@ __device__ __forceinline__ uint32_t pack_children_wave(const uint32_t* hist, uin
                 base = s_ex + sinc[j];
             }
             const uint32_t P = s_ex + sinc[j] - (small ? m[j] : 0u) - base;  // run-relative start
-            key[j] = small ? (run << 12) + (P >> 8) + 1u : 0u;  // P < 2^20: P >> 8 < 4096
+            key[j] = small ? (run << 14) + (P >> kWin) + 1u : 0u;  // P < 2^20: P >> kWin < 2^14
             kmax = key[j] > kmax ? key[j] : kmax;
         }
         uint32_t prevk = lane_prev(wave_incl_max(kmax), 0u);
         uint32_t st[4], nst = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const bool mid = m[j] > kHalf && m[j] <= (uint32_t)kSmall;
+            const bool mid = m[j] > kHalf && m[j] <= (uint32_t)SMALL;
             st[j] = (key[j] && key[j] != prevk) || mid;
             if (key[j]) prevk = key[j];
             nst += st[j];
@@ -1557,7 +1571,7 @@ __device__ __forceinline__ uint32_t pack_children_wave(const uint32_t* hist, uin
         uint32_t idx = st_ex;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const bool member = key[j] || (m[j] > kHalf && m[j] <= (uint32_t)kSmall);
+            const bool member = key[j] || (m[j] > kHalf && m[j] <= (uint32_t)SMALL);
             if (st[j]) {
                 bat_start[idx] = pos_ex + pos[j];
                 idx++;
@@ -2395,7 +2409,7 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
 __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restrict__ blocks, size_t stride,
                                                         const uint32_t* __restrict__ lens,
                                                         uint32_t* __restrict__ sa_all, uint8_t* __restrict__ bwt_out,
-                                                        uint32_t* __restrict__ orig_out, uint8_t* scratch,
+                                                        uint32_t* __restrict__ orig_out, uint8_t* scratch, uint32_t* __restrict__ spill_all,
                                                         size_t scratch_per_slot, int S, const BwtItem* __restrict__ lin,
                                                         const uint32_t* __restrict__ lin_count, BwtItem* __restrict__ lout,
                                                         uint32_t* __restrict__ lout_count, size_t lcap,
@@ -2406,12 +2420,12 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
     __shared__ LevelLds L;
     const uint32_t nin = shard_index_load(lin_count, L.si);
     if (nin == 0) return;
-    // slot scratch (bwt_level_slot_bytes): spill area, then the local lists
+    // slot scratch (bwt_level_slot_bytes): the local lists; a segment's spill
+    // area is its own range of the block's per-rotation spill (segments of a
+    // level, and sub-segments of one, are disjoint ranges of the SA)
     Scratch s{};
     {
         uint8_t* p = scratch + (size_t)blockIdx.x * scratch_per_slot;
-        s.vb = (uint32_t*)p;
-        p += 4 * (size_t)S;
         s.large = (Seg*)p;
         p += 8 * ((size_t)S / kSmall + 8);
         s.large2 = (Seg*)p;
@@ -2438,8 +2452,9 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
         const GroupSink sink{grp_all + (size_t)b * bwt_group_stride(stride), &ngroups[b], 0xffffffffu, p2list,
                              p2count, b, nullptr, nullptr};
         uint32_t d = uniform(it.depth);
+        uint32_t* spill = spill_all + (size_t)b * stride;
         if (!last) {
-            partition_segment(T, n, b, sa, Seg{it.start, it.len}, d, L, s.vb, sq,
+            partition_segment(T, n, b, sa, Seg{it.start, it.len}, d, L, spill + it.start, sq,
                               GlobalLarge{Sharded<BwtItem>{lout, lout_count, lcap}}, sink, bw, orig_out + b, pt);
             continue;
         }
@@ -2457,7 +2472,7 @@ __global__ __launch_bounds__(256) void bwt_level_kernel(const uint8_t* __restric
             if (t == 0) L.sh.cnt[3] = 0;
             __syncthreads();
             for (uint32_t k = 0; k < nc; ++k)
-                partition_segment(T, n, b, sa, cur[k], d, L, s.vb, sq, LocalLarge{nxt, &L.sh.cnt[3]}, sink, bw,
+                partition_segment(T, n, b, sa, cur[k], d, L, spill + cur[k].start, sq, LocalLarge{nxt, &L.sh.cnt[3]}, sink, bw,
                                   orig_out + b, pt);
             if (t == 0) L.sh.cnt[1] = L.sh.cnt[3];
             __syncthreads();
@@ -2697,6 +2712,14 @@ constexpr int kTextTieCap = BZ2MI_TEXT_TIECAP;  // tie depth after which a wave 
 #define BZ2MI_TEXT_PAIRCAP 32
 #endif
 constexpr int kTextPairCap = BZ2MI_TEXT_PAIRCAP;  // depth to which two tied rotations are compared directly
+// largest segment the text kernel sorts in one wave (A/B: -DBZ2MI_TEXT_SMALL=512):
+// 256 keeps every sort at <= 4 keys per lane, so the kernel's state fits the
+// 128 VGPRs of a 1024-thread workgroup; larger segments are partitioned
+#ifndef BZ2MI_TEXT_SMALL
+#define BZ2MI_TEXT_SMALL 256
+#endif
+constexpr int kTS = BZ2MI_TEXT_SMALL;
+static_assert(kTS == 256 || kTS == 512, "text sort size");
 constexpr int kTQ = 512;          // work items per round
 constexpr int kCopyR = 4;         // rotations per lane and chunk of a copy step
 constexpr int kTW = 768;          // per-wave LDS words
@@ -2832,7 +2855,7 @@ __device__ __forceinline__ void tq_push(TextLds& L, int nxt, bool want, uint32_t
 // Work of an item for the dealing: a sort ~ its padded size, a partition ~ half
 // its length (one pass, the children are items of their own)
 __device__ __forceinline__ uint32_t text_work(uint32_t len) {
-    return len > (uint32_t)kSmall ? (len >> 1) : len <= 64u ? 64u : len <= 128u ? 128u : len <= 256u ? 256u : 512u;
+    return len > (uint32_t)kTS ? (len >> 1) : len <= 64u ? 64u : len <= 128u ? 128u : len <= 256u ? 256u : 512u;
 }
 // the wave of an item whose work starts at `run` (of `total`): equal shares
 __device__ __forceinline__ uint8_t text_owner(uint32_t run, uint32_t wk, uint32_t total) {
@@ -2896,7 +2919,7 @@ __device__ __forceinline__ int text_cmp_deferred(const uint8_t* Tl, int n, uint3
 __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_t* sa, uint32_t base, uint32_t tt,
                                                uint32_t D, uint8_t* out, uint32_t* orig, uint32_t* W, TextLds& L,
                                                uint64_t* dl) {
-    constexpr int E = kSmall / 64;
+    constexpr int E = kTS / 64;
     const int lane = lane_id();
     uint32_t wv[E];
     bool keep[E], ph[E];
@@ -2973,7 +2996,7 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
     return tot;
 }
 
-// sort a segment of <= kSmall rotations with a common prefix of d bytes (one
+// sort a segment of <= kTS rotations with a common prefix of d bytes (one
 // wave; keys from the LDS text); final SA entries, BWT bytes, origPtr.  Items
 // still tied after kTextTieCap bytes keep their slots with the kUnres flag
 // (ordered by the resolve pass).
@@ -2997,17 +3020,17 @@ constexpr bool kTextPrefetch = BZ2MI_TEXT_PREFETCH != 0;
 #endif
 __device__ TBK_SORT_INL void text_sort_pre(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out,
                                             uint32_t* orig, uint32_t* W, TextLds& L, uint64_t* dl,
-                                            const uint32_t (&pre)[kSmall / 64]) {
+                                            const uint32_t (&pre)[kTS / 64]) {
     const int lane = lane_id();
-    TBK_ASSERT(seg.start + seg.len <= (uint32_t)n && seg.len >= 2u && seg.len <= (uint32_t)kSmall, "sort seg", seg.start,
+    TBK_ASSERT(seg.start + seg.len <= (uint32_t)n && seg.len >= 2u && seg.len <= (uint32_t)kTS, "sort seg", seg.start,
                seg.len);
     Scratch s{};
     s.sa = sa;
     uint32_t tt;
     if (seg.len <= 64) tt = wave_sort_pre_text<1>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
     else if (seg.len <= 128) tt = wave_sort_pre_text<2>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
-    else if (seg.len <= 256) tt = wave_sort_pre_text<4>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
-    else tt = wave_sort_pre_text<8>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    else if (kTS <= 256 || seg.len <= 256) tt = wave_sort_pre_text<kTS <= 256 ? kTS / 64 : 4>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    else tt = wave_sort_pre_text<kTS / 64>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
     tt = uniform(tt);
     TBK_COUNT(4, 1);
     TBK_COUNT(7, seg.len);
@@ -3036,14 +3059,14 @@ __device__ TBK_SORT_INL void text_sort_pre(const uint8_t* Tl, int n, uint32_t* s
             if (lane == 0) atomicAdd(&L.nflag, tt);
             return;
         }
-        tt = uniform(lds_tie_round_any(Tl, n, s, seg.start, tt, D, out, orig, W));
+        tt = uniform(lds_tie_round_upto<kTS / 64>(Tl, n, s, seg.start, tt, D, out, orig, W));
         D += kLdsTieBytes;
     }
 }
 
 __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, Seg seg, uint32_t d, uint8_t* out,
                                         uint32_t* orig, uint32_t* W, TextLds& L, uint64_t* dl) {
-    constexpr int E = kSmall / 64;
+    constexpr int E = kTS / 64;
     const int lane = lane_id();
     uint32_t pre[E];
 #pragma unroll
@@ -3054,7 +3077,7 @@ __device__ TBK_SORT_INL void text_sort(const uint8_t* Tl, int n, uint32_t* sa, S
     text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
 }
 
-// partition a segment of > kSmall rotations with a common prefix of d bytes
+// partition a segment of > kTS rotations with a common prefix of d bytes
 // by byte d (one wave): children of one rotation are final, runs of small
 // ones go to the queue as batches, large ones as items of depth d+1.  A
 // segment that is still one child kTextChain levels down (or at kTextDcap) is
@@ -3066,11 +3089,11 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     uint32_t* base = W + 256;  // then pack scratch / the batch lengths
     constexpr int U = 8;
     const uint32_t rounds = (seg.len + 63) / 64;
-    TBK_ASSERT(seg.start + seg.len <= (uint32_t)n && seg.len > (uint32_t)kSmall, "partition seg", seg.start, seg.len);
+    TBK_ASSERT(seg.start + seg.len <= (uint32_t)n && seg.len > (uint32_t)kTS, "partition seg", seg.start, seg.len);
     uint32_t c[4];
     const uint32_t dcap = min((uint32_t)kTextDcap, d + (uint32_t)kTextChain);
     for (;;) {
-        if (d >= dcap) {  // more than kSmall rotations sharing d bytes: the general path
+        if (d >= dcap) {  // more than kTS rotations sharing d bytes: the general path
             if (lane == 0) TBK_FAIL(5);
             return;
         }
@@ -3143,7 +3166,7 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     }
     wave_sync_mem();  // the scatter is visible to the reads below
     // batches of the small children (pack scratch: the hist and base areas)
-    const uint32_t nbat = pack_children_wave(hist, base, W + 512, hist, base);
+    const uint32_t nbat = pack_children_wave<kTS>(hist, base, W + 512, hist, base);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         if (c[j] == 1u) {
@@ -3153,7 +3176,7 @@ __device__ TBK_PART_INL void text_partition(const uint8_t* Tl, int n, uint32_t* 
     }
     bool big[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) big[j] = c[j] > (uint32_t)kSmall;
+    for (int j = 0; j < 4; ++j) big[j] = c[j] > (uint32_t)kTS;
 #pragma unroll
     for (int j = 0; j < 4; ++j) tq_push(L, nxt, big[j], seg.start + ex[j], c[j], d + 1);
     for (uint32_t k0 = 0; k0 < nbat; k0 += 64) {
@@ -3222,21 +3245,32 @@ __device__ __forceinline__ int text_cmp_plain(const uint8_t* Tl, int n, uint32_t
 
 // Rank of member k of deferred group g whose members' rotations i + x all
 // have known positions (isa): the members keep the order of their images.
-// Serial over the m members (m <= 64; nearly always 2 or 3).
+// Serial over the m members (m <= 64; nearly always 2 or 3), with no local
+// arrays (they went to scratch): the ranks by counting over reloaded images
+// (isa of the members themselves -- their new slots, set in the first loop --
+// is never an image: an image is placed, a member is not), then the SA slots
+// permuted in place by following cycles.
 __device__ __forceinline__ void dg_place_by_images(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa,
                                                    uint8_t* out, uint32_t* orig, uint32_t st, uint32_t m,
                                                    uint32_t x) {
-    uint32_t mem[64], key[64];
+    auto image = [&](uint32_t k) { return isa[((ld_fresh(sa + st + k) & 0x1ffffu) + x) % (uint32_t)n]; };
     for (uint32_t k = 0; k < m; ++k) {
-        mem[k] = ld_fresh(sa + st + k) & 0x1ffffu;
-        key[k] = isa[(mem[k] + x) % (uint32_t)n];
-    }
-    for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t mk = ld_fresh(sa + st + k) & 0x1ffffu, key = image(k);
         uint32_t r = 0;
-        for (uint32_t j = 0; j < m; ++j) r += key[j] < key[k] ? 1u : 0u;
-        sa[st + r] = mem[k];
-        isa[mem[k]] = st + r;
-        text_final(Tl, n, st + r, mem[k], out, orig);
+        for (uint32_t j = 0; j < m; ++j) r += image(j) < key ? 1u : 0u;
+        isa[mk] = st + r;
+        text_final(Tl, n, st + r, mk, out, orig);
+    }
+    for (uint32_t q = 0; q < m; ++q) {
+        uint32_t v = ld_fresh(sa + st + q) & 0x1ffffu;
+        uint32_t to = isa[v] - st;
+        while (to != q) {
+            const uint32_t w = ld_fresh(sa + st + to) & 0x1ffffu;
+            sa[st + to] = v;
+            v = w;
+            to = isa[v] - st;
+        }
+        sa[st + q] = v;
     }
 }
 
@@ -3685,7 +3719,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     __syncthreads();
     // sort items (dl2, free until the deferred groups are sorted): a thread
     // per first-byte row walks its pair buckets in order; runs of consecutive
-    // explicit pairs of <= kSmall / 2 rotations become batches of <= kSmall
+    // explicit pairs of <= kTS / 2 rotations become batches of <= kTS
     // (sorted from depth 1: the second byte separates them), larger pairs
     // items of their own (depth 2: a wave sort or a partition); explicit
     // pairs of one rotation are final.  (cnt[j] is pair j's end after the
@@ -3710,12 +3744,12 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                     flush();
                     continue;
                 }
-                if (len > (uint32_t)kSmall / 2) {
+                if (len > (uint32_t)kTS / 2) {
                     flush();
                     dl2[atomicAdd(&L.nitems, 1u)] = tq_item(st, len, 2u);
                     continue;
                 }
-                if (blen + len > (uint32_t)kSmall) flush();
+                if (blen + len > (uint32_t)kTS) flush();
                 if (blen == 0) bst = st;
                 blen += len;
                 bcnt++;
@@ -3736,7 +3770,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         const uint32_t k = uniform(kk);
         if (k >= nitems || guard > nitems) break;
         if (uniform(*(volatile uint32_t*)&L.fail)) break;
-        constexpr int E = kSmall / 64;
+        constexpr int E = kTS / 64;
         uint32_t pre[E];
         const uint64_t it = dl2[k];
         const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
@@ -3744,10 +3778,10 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t g = (uint32_t)(e * 64 + lane);
-            pre[e] = (seg.len <= (uint32_t)kSmall && g < seg.len) ? ld_fresh(sa + seg.start + g) : 0u;
+            pre[e] = (seg.len <= (uint32_t)kTS && g < seg.len) ? ld_fresh(sa + seg.start + g) : 0u;
         }
         TBK_T(2, seg.len);
-        if (seg.len <= (uint32_t)kSmall) text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
+        if (seg.len <= (uint32_t)kTS) text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
         else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, 0);
         TBK_T(10, k);
     }
@@ -3778,7 +3812,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         // this wave's items, the next one's SA entries loaded while the
         // current one is sorted
         const uint32_t lo = uniform(L.wlo[w]), hi = uniform(L.whi[w]);
-        constexpr int E = kSmall / 64;
+        constexpr int E = kTS / 64;
         uint32_t pre[E];
         auto load = [&](uint32_t k, uint32_t (&dst)[E]) {
             const uint64_t it = dl2[k];
@@ -3786,7 +3820,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 const uint32_t g = (uint32_t)(e * 64 + lane);
-                dst[e] = (len <= (uint32_t)kSmall && g < len) ? ld_fresh(sa + st + g) : 0u;
+                dst[e] = (len <= (uint32_t)kTS && g < len) ? ld_fresh(sa + st + g) : 0u;
             }
         };
         if (kTextPrefetch && lo < hi) load(lo, pre);
@@ -3802,11 +3836,11 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
             const unsigned long long ti0 = wall_clock64();
 #endif
-            if (seg.len <= (uint32_t)kSmall) text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
+            if (seg.len <= (uint32_t)kTS) text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
             else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, 0);
             TBK_T(10, seg.len);
 #ifdef BZ2MI_PHASES
-            TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
+            TBK_COUNT(seg.len <= (uint32_t)kTS ? 12 : 13, wall_clock64() - ti0);
 #endif
             if (kTextPrefetch) {
 #pragma unroll
@@ -3856,11 +3890,11 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
             const unsigned long long ti0 = wall_clock64();
 #endif
-            if (seg.len <= (uint32_t)kSmall) text_sort(Tl, n, sa, seg, d, out, orig, W, L, dl);
+            if (seg.len <= (uint32_t)kTS) text_sort(Tl, n, sa, seg, d, out, orig, W, L, dl);
             else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, cur ^ 1);
             TBK_T(11, seg.len);
 #ifdef BZ2MI_PHASES
-            TBK_COUNT(seg.len <= (uint32_t)kSmall ? 12 : 13, wall_clock64() - ti0);
+            TBK_COUNT(seg.len <= (uint32_t)kTS ? 12 : 13, wall_clock64() - ti0);
 #endif
             }
         }

@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -27,6 +28,16 @@ inline int fail(int code, const std::string& msg) { return bz2mi_set_error(code,
             return ::bz2mi::host::fail(BZ2MI_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// BZ2MI_DEBUG_MAX_ALLOC=<bytes> (tests): any larger device allocation fails
+// as if HBM were short, to exercise the callers' fallbacks
+inline size_t debug_max_alloc() {
+    static size_t v = [] {
+        const char* e = getenv("BZ2MI_DEBUG_MAX_ALLOC");
+        return (e && *e) ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
+    }();
+    return v;
+}
+
 template <class T>
 int dalloc(T** p, size_t count) {
     if (*p) {
@@ -34,6 +45,8 @@ int dalloc(T** p, size_t count) {
         *p = nullptr;
     }
     if (count == 0) count = 1;
+    if (debug_max_alloc() && count * sizeof(T) > debug_max_alloc())
+        return fail(BZ2MI_EDEVICE, "hipMalloc: out of memory (BZ2MI_DEBUG_MAX_ALLOC)");
     hipError_t e = hipMalloc((void**)p, count * sizeof(T));
     if (e != hipSuccess) {
         *p = nullptr;

@@ -9,8 +9,9 @@ namespace bz2mi {
 
 // Scratch bytes one BWT workgroup slot needs for blocks of S bytes.
 inline size_t bwt_slot_bytes(int S) { return (size_t)48 * (size_t)S + 4096; }
-// ... and one bwt_level_kernel workgroup slot (spill area + two segment lists)
-inline size_t bwt_level_slot_bytes(int S) { return (size_t)4 * (size_t)S + 16 * ((size_t)S / 512 + 8) + 256; }
+// ... and one bwt_level_kernel workgroup slot (two segment lists; the spill
+// area is the block's per-rotation spill, d_lspill)
+inline size_t bwt_level_slot_bytes(int S) { return 16 * ((size_t)S / 512 + 8) + 256; }
 
 // BWT (bwt.hip): per-block counting sort by the first byte; levels of
 // partitions by the next byte for the large buckets of all blocks at once
@@ -62,8 +63,8 @@ __global__ void bwt_text_kernel(const uint8_t* blocks, size_t stride, const uint
                                 size_t tcap);
 __global__ void redo_all_kernel(uint32_t* redo, int nblocks);
 __global__ void bwt_level_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
-                                 uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, size_t scratch_per_slot,
-                                 int S, const BwtItem* lin, const uint32_t* lin_count, BwtItem* lout,
+                                 uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, uint32_t* spill_all,
+                                 size_t scratch_per_slot, int S, const BwtItem* lin, const uint32_t* lin_count, BwtItem* lout,
                                  uint32_t* lout_count, size_t lcap, uint64_t* squeue, uint32_t* scount, size_t scap,
                                  BwtSeg* grp_all, uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count, int last,
                                  uint32_t smask);

@@ -12,6 +12,7 @@ import bz2
 import ctypes
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -299,26 +300,29 @@ def test_900k_mode_random_1gib_matches_cpuref(bz, cpuref):
 
 
 def test_900k_mode_under_memory_pressure(bz, cpuref):
-    """Most of HBM held by another allocation (all but 8 GiB): the 900 KB mode
-    sizes its batches from the free memory (several batches), and a batch
-    that still does not fit (forced with a batch far above what is left) is
-    halved until it does; the stream stays the C restatement's."""
+    """Most of HBM held by another allocation (all but 16 GiB): the 900 KB
+    mode sizes its batches from the free memory (several batches instead of
+    one); and with every device allocation above 1 GiB made to fail
+    (BZ2MI_DEBUG_MAX_ALLOC), the batches are halved until they fit.  The
+    stream stays the C restatement's."""
     import torch
     from bz2mi import synth
+    data = synth.random_bytes(256 << 20).tobytes()
+    want = cpuref.compress(data, 9, 10, unit=100000, threads=16)
     free, _total = torch.cuda.mem_get_info()
-    hold = torch.empty(max(0, free - (8 << 30)), dtype=torch.uint8, device="cuda")
+    hold = torch.empty(max(0, free - (16 << 30)), dtype=torch.uint8, device="cuda")
     try:
-        data = synth.random_bytes(256 << 20).tobytes()
-        want = cpuref.compress(data, 9, 10, unit=100000, threads=16)
         assert bz.compress(data, 9, 10, unit=100000) == want
-        os.environ["BZ2MI_BATCH_BLOCKS"] = "100000"
-        try:
-            got = bz.compress(data, 9, 10, unit=100000)
-        finally:
-            del os.environ["BZ2MI_BATCH_BLOCKS"]
-        assert got == want
         text = synth.realtext_bytes(24 << 20).tobytes()
         assert bz.compress(text, 9, 10, unit=100000) == cpuref.compress(text, 9, 10, unit=100000, threads=16)
     finally:
         del hold
         torch.cuda.empty_cache()
+    os.environ["BZ2MI_DEBUG_MAX_ALLOC"] = str(1 << 30)
+    try:
+        got = subprocess.run([sys.executable, "-c", "import sys, bz2mi; d = sys.stdin.buffer.read(); "
+                              "sys.stdout.buffer.write(bz2mi.compress(d, 9, 10, unit=100000))"],
+                             input=data, capture_output=True, cwd=os.path.join(PKG), check=True).stdout
+    finally:
+        del os.environ["BZ2MI_DEBUG_MAX_ALLOC"]
+    assert got == want
