@@ -55,9 +55,14 @@ def ensure_built():
         subprocess.run(["make", "-C", PKG, "-j8"], check=True, stdout=subprocess.DEVNULL)
 
 
-TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r04_traffic_{data}.json")
-ISSUE_PROFILE = os.path.join(REPO, "profiles", "r04_issue_{data}.json")
-KSTATS_PROFILE = "profiles/r04_kernel_stats_{data}_v3.csv"
+# committed rocprofv3 passes of this same command (tools/r5_measure.sh):
+# traffic (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic.py), issue (SQ/GRBM
+# counters, tools/issue.py) and kernel stats; each file records the sha256 of
+# the library it was measured with, and a file from another build is not used
+PROFILE_ROUND = "r05"
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", PROFILE_ROUND + "_traffic_{name}.json")
+ISSUE_PROFILE = os.path.join(REPO, "profiles", PROFILE_ROUND + "_issue_{name}.json")
+KSTATS_PROFILE = "profiles/" + PROFILE_ROUND + "_kernel_stats_{name}.csv"
 # the kernels of each timed stage (bz2mi_compress_device, csrc/api.hip)
 STAGE_KERNELS = {
     "front": "fe_summary/runscan/costscan/dmap/chain/resolve (scans + block chain) and fe_rle1_kernel",
@@ -71,48 +76,109 @@ STAGE_KERNELS = {
 }
 
 
-def stage_traffic(args, stage):
-    """HBM-side bytes per launch of `stage` from the committed rocprofv3 --pmc
-    passes of this same command (tools/measure.sh -> tools/traffic.py:
-    FETCH_SIZE x2 per the gfx950 note of MI355X_MICROARCH.md, + WRITE_SIZE).
-    Only for the workloads those passes ran (1 GiB of --data random/text at the
-    default level/p/unit; tools/measure.sh)."""
-    if args.mib != 1024 or args.level != 9 or args.parallel != 10 or args.unit != 10000:
-        return None, None
-    path = TRAFFIC_PROFILE.format(data=args.data)
+def lib_sha16() -> str | None:
+    """sha256 (16 hex digits) of the library this process loads."""
+    import hashlib
+    path = os.environ.get("BZ2MI_LIBRARY") or os.path.join(PKG, "bz2mi", "libbz2mi.so")
     try:
-        with open(path) as f:
-            prof = json.load(f)
-        return int(prof["stages"][stage]["traffic_bytes"]), os.path.relpath(path, REPO)
-    except (OSError, KeyError, ValueError):
-        return None, None
-
-
-ISSUE_PREFIX = {"front": ("fe_",), "bwt": ("bwt_",), "mtf": ("mtf_kernel",), "huffman": ("huffman_kernel",),
-                "assemble": ("assemble", "offsets_dev", "advance")}
-
-
-def stage_issue(args, stage):
-    """VALU issue utilisation and LDS bank-conflict share of the stage's
-    kernels, from the committed SQ/GRBM --pmc pass of this same command
-    (tools/r4_measure.sh -> tools/issue.py); kernels taking <2% of the stage's
-    profiled time are left out."""
-    if args.mib != 1024 or args.level != 9 or args.parallel != 10 or args.unit != 10000:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
         return None
-    path = ISSUE_PROFILE.format(data=args.data)
+
+
+def profile_name(data: str, unit: int) -> str:
+    return data + ("900k" if unit == 100000 else "")
+
+
+def _profile(path: str):
+    """A committed profile of this build: (json, relpath, None) or (None, relpath, why)."""
+    rel = os.path.relpath(path, REPO)
     try:
         with open(path) as f:
             prof = json.load(f)
     except (OSError, ValueError):
+        return None, rel, "no profile"
+    sha = lib_sha16()
+    if prof.get("lib_sha16") != sha:
+        return None, rel, f"measured with library {prof.get('lib_sha16')}, this run loads {sha}"
+    return prof, rel, None
+
+
+def default_shape(args) -> bool:
+    return args.mib == 1024 and args.level == 9 and args.parallel == 10
+
+
+def stage_traffic(args, stage, unit):
+    """HBM-side bytes per launch of `stage` from the committed rocprofv3 --pmc
+    passes of this same command and build (FETCH_SIZE x2 per the gfx950 note of
+    MI355X_MICROARCH.md, + WRITE_SIZE).  Only for the workloads those passes
+    ran (1 GiB at -9, p = 10)."""
+    if not default_shape(args):
+        return None, None, "not a profiled workload"
+    prof, rel, why = _profile(TRAFFIC_PROFILE.format(name=profile_name(args.data, unit)))
+    if prof is None:
+        return None, rel, why
+    try:
+        return int(prof["stages"][stage]["traffic_bytes"]), rel, None
+    except (KeyError, ValueError):
+        return None, rel, "stage missing"
+
+
+ISSUE_PREFIX = {"front": ("fe_",), "bwt": ("bwt_", "dbl_"), "mtf": ("mtf_kernel",), "huffman": ("huffman_kernel",),
+                "assemble": ("assemble", "offsets_dev", "advance")}
+
+
+def stage_issue(args, stage, unit):
+    """VALU issue utilisation and LDS bank-conflict share of the stage's
+    kernels, from the committed SQ/GRBM --pmc pass of this same command and
+    build (tools/issue.py); kernels taking <2% of the stage's profiled time
+    are left out."""
+    if not default_shape(args):
         return None
+    prof, rel, why = _profile(ISSUE_PROFILE.format(name=profile_name(args.data, unit)))
+    if prof is None:
+        return {"source": rel, "unavailable": why}
     ks = {k: v for k, v in prof["kernels"].items() if k.startswith(ISSUE_PREFIX[stage])}
     tot = sum(v["ms_total"] for v in ks.values()) or 1.0
     keep = {k: {a: v[a] for a in ("valu_issue_frac", "lds_bank_conflict_frac", "salu_per_valu", "eff_clock_GHz")
                 if a in v} | {"time_share": round(v["ms_total"] / tot, 3)}
             for k, v in ks.items() if v["ms_total"] >= 0.02 * tot}
-    return {"source": os.path.relpath(path, REPO), "kernels": keep,
+    return {"source": rel, "kernels": keep,
             "what": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE/8): the share of SIMD issue "
                     "slots the kernel's VALU stream used; SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE"}
+
+
+def roofline(args, unit, n, stats, avg, out_len, ms_step):
+    """The dominant stage against the HBM roofline: algorithmic bytes per
+    launch (DESIGN.md "Roofline") / its HIP-event time, the committed traffic
+    and issue passes of this build, the pipeline rate."""
+    rle1 = stats["rle1_bytes"]
+    syms = stats["mtf_symbols"]
+    payload = stats["payload_bits"] // 8
+    nb = stats["blocks"]
+    alg = {
+        "front": 2 * n + rle1,                       # read input twice (scan + emission), write RLE1 blocks
+        "bwt": 2 * rle1 + 4 * nb,                    # read block, write BWT (+ origPtr)
+        "mtf": rle1 + 2 * syms + 258 * 4 * nb,       # read BWT, write u16 symbols + histogram
+        "huffman": 2 * syms + payload,               # read symbols, write payload
+        "assemble": payload + out_len,               # read payload, write stream
+    }
+    dom = max((k for k in alg if avg.get(k, 0) > 0), key=lambda k: avg[k])
+    achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9
+    traffic, tsrc, why = stage_traffic(args, dom, unit)
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            "traffic_unavailable": why,
+            "algorithmic_bytes": int(alg[dom]), "avg_ms": round(avg[dom], 3),
+            "stage_kernels": STAGE_KERNELS.get(dom),
+            "issue": stage_issue(args, dom, unit),
+            "lib_sha16": lib_sha16(),
+            "what": "HIP events around the stage's launches on the stream they run on, per step; the stage is "
+                    "the kernels listed (their rocprofv3 durations sum to avg_ms: "
+                    + KSTATS_PROFILE.format(name=profile_name(args.data, unit)) + ")",
+            "pipeline_GBps": round((n + out_len) / (ms_step * 1e-3) / 1e9, 2),
+            "stage_ms": {k: round(v, 3) for k, v in avg.items()}}
 
 
 def host_cpu() -> dict:
@@ -353,31 +419,8 @@ def main():
     ms_step = dt / steps * 1e3
     value = world * n * steps / dt / 1e6
     avg = {k: v / steps for k, v in stage_sum.items()}
-    # algorithmic bytes per launch of each stage (DESIGN.md "Roofline")
-    rle1 = stats["rle1_bytes"]
-    syms = stats["mtf_symbols"]
-    payload = stats["payload_bits"] // 8
     nb = stats["blocks"]
-    alg = {
-        "front": 2 * n + rle1,                       # read input twice (scan + emission), write RLE1 blocks
-        "bwt": 2 * rle1 + 4 * nb,                    # read block, write BWT (+ origPtr)
-        "mtf": rle1 + 2 * syms + 258 * 4 * nb,       # read BWT, write u16 symbols + histogram
-        "huffman": 2 * syms + payload,               # read symbols, write payload
-        "assemble": payload + out_len,               # read payload, write stream
-    }
-    dom = max((k for k in alg if avg.get(k, 0) > 0), key=lambda k: avg[k])
-    achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9
-    traffic, tsrc = stage_traffic(args, dom)
-    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-            "algorithmic_bytes": int(alg[dom]), "avg_ms": round(avg[dom], 3),
-            "stage_kernels": STAGE_KERNELS.get(dom),
-            "issue": stage_issue(args, dom),
-            "what": "HIP events around the stage's launches on the stream they run on, per step; the stage is "
-                    "the kernels listed (their rocprofv3 durations sum to avg_ms: "
-                    + KSTATS_PROFILE.format(data=args.data) + ")",
-            "pipeline_GBps": round((n + out_len) / (ms_step * 1e-3) / 1e9, 2),
-            "stage_ms": {k: round(v, 3) for k, v in avg.items()}}
+    roof = roofline(args, args.unit, n, stats, avg, out_len, ms_step)
     # the metric's literal wording, "900KB blocks": the same input at -9 in the
     # 900 KB mode (unit 100000, S = 900,000; O_ref900 pins),
     # timed the same way right after the line's own steps
@@ -413,10 +456,12 @@ def main():
                 ok9 = bool(len(got9) > 0 and got9 == x[: len(got9)].cpu().numpy().tobytes())
             except Exception:
                 ok9 = False
+        stats9 = ctx9.stats()
+        ms9 = dt9 / args.steps * 1e3
         mode900 = {"value": round(n * args.steps / dt9 / 1e6, 2), "unit": "MB/s",
-                   "ms_per_step": round(dt9 / args.steps * 1e3, 3), "block_size": args.level * 100000,
-                   "blocks": ctx9.stats()["blocks"], "output_bytes": int(z9), "decode_check": ok9,
-                   "stage_ms": {k: round(v / args.steps, 3) for k, v in st9.items()},
+                   "ms_per_step": round(ms9, 3), "block_size": args.level * 100000,
+                   "blocks": stats9["blocks"], "output_bytes": int(z9), "decode_check": ok9,
+                   "roofline": roofline(args, 100000, n, stats9, {k: v / args.steps for k, v in st9.items()}, z9, ms9),
                    "what": "the same input and steps at -9 in the 900 KB mode (unit 100000; O_ref900 pins)"}
         del out9
         ctx9.close()

@@ -2746,7 +2746,8 @@ struct TextLds {
     uint32_t cstart[257];             // first-byte bucket starts
     uint32_t tmp[FW];
     uint32_t wlo[FW], whi[FW];        // a wave's range of pair entries (the deal)
-    uint32_t qn[2], fail, nflag, ndef, nitems, next_item;
+    uint32_t qn[2], fail, nflag, ndef, nitems, next_item;  // next_item: the work queue's next dl2 item
+    uint32_t wq_head, wq_tail, wq_used, wq_out;  // work queue (BZ2MI_TEXT_WQ): claimed, reserved, read, unfinished
     uint8_t order[256];               // bytes by ascending bucket size
     uint8_t rank[256];                // position of a byte in that order
     uint8_t target[256];
@@ -2795,10 +2796,37 @@ __device__ __forceinline__ uint64_t tq_item(uint32_t start, uint32_t len, uint32
 
 // append the items of the lanes with `want` to the next round's list
 // (wave-aggregated); a full list means the block gives up
+// the work queue of BZ2MI_TEXT_WQ builds: a ring over L.q (2 * kTQ entries);
+// an entry is an item with bit 63 set (0: empty), the ring positions grow
+// without bound (slot = position mod the ring size)
+constexpr uint32_t kWqRing = 2 * kTQ;
+constexpr uint64_t kWqValid = 1ull << 63;
+constexpr int kWqPush = 2;  // tq_push's `nxt` for the ring
+
 __device__ __forceinline__ void tq_push(TextLds& L, int nxt, bool want, uint32_t start, uint32_t len,
                                         uint32_t depth) {
     const uint64_t m = __ballot(want);
     if (m == 0) return;
+    if (nxt == kWqPush) {
+        // unfinished count first (a waiting wave must not see 0 while these
+        // items exist), then the slots; a ring that would overrun the slots
+        // not yet read sends the block back
+        uint32_t base = 0, over = 0;
+        if (lane_id() == 0) {
+            const uint32_t c = (uint32_t)__popcll(m);
+            atomicAdd(&L.wq_out, c);
+            base = atomicAdd(&L.wq_tail, c);
+            over = base + c - *(volatile uint32_t*)&L.wq_used > kWqRing ? 1u : 0u;
+            if (over) TBK_FAIL(4);
+        }
+        base = uniform(base);
+        if (uniform(over)) return;  // (the block goes back; the slots are not written)
+        if (want) {
+            const uint32_t pos = base + (uint32_t)__popcll(m & __lanemask_lt());
+            (&L.q[0][0])[pos % kWqRing] = tq_item(start, len, depth) | kWqValid;
+        }
+        return;
+    }
     uint32_t base = 0;
     if (lane_id() == 0) base = atomicAdd(&L.qn[nxt], (uint32_t)__popcll(m));
     base = uniform(base);
@@ -3009,10 +3037,10 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
 #ifndef BZ2MI_TEXT_PREFETCH
 #define BZ2MI_TEXT_PREFETCH 0
 #endif
-// A/B: round-0 sort items pulled by the waves from an LDS counter instead of
-// the static deal
-#ifndef BZ2MI_TEXT_DYNDEAL
-#define BZ2MI_TEXT_DYNDEAL 0
+// the whole sort phase as one work queue (no rounds; A/B: -DBZ2MI_TEXT_WQ=0
+// = the round-4 static deal and barrier-separated rounds)
+#ifndef BZ2MI_TEXT_WQ
+#define BZ2MI_TEXT_WQ 1
 #endif
 constexpr bool kTextPrefetch = BZ2MI_TEXT_PREFETCH != 0;
 #ifndef TBK_PART_INL
@@ -3760,31 +3788,68 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     __threadfence_block();
     __syncthreads();
     const uint32_t nitems = uniform(L.nitems);
-#if BZ2MI_TEXT_DYNDEAL
-    // A/B: every wave pulls its next item from an LDS counter
-    if (t == 0) L.next_item = 0;
-    __syncthreads();
-    for (uint32_t guard = 0;; ++guard) {
-        uint32_t kk = 0;
-        if (lane == 0) kk = atomicAdd(&L.next_item, 1u);
-        const uint32_t k = uniform(kk);
-        if (k >= nitems || guard > nitems) break;
-        if (uniform(*(volatile uint32_t*)&L.fail)) break;
-        constexpr int E = kTS / 64;
-        uint32_t pre[E];
-        const uint64_t it = dl2[k];
-        const Seg seg{uniform((uint32_t)it & 0x1ffffu), uniform((uint32_t)(it >> 17) & 0x1ffffu)};
-        const uint32_t d = uniform((uint32_t)(it >> 34) & 0xffffu);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const uint32_t g = (uint32_t)(e * 64 + lane);
-            pre[e] = (seg.len <= (uint32_t)kTS && g < seg.len) ? ld_fresh(sa + seg.start + g) : 0u;
-        }
-        TBK_T(2, seg.len);
-        if (seg.len <= (uint32_t)kTS) text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
-        else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, 0);
-        TBK_T(10, k);
+#if BZ2MI_TEXT_WQ
+    // One work queue for the whole sort phase, no rounds: a wave takes the
+    // oldest item of the ring (children of partitions) or else the next sort
+    // item of dl2, and pushes a partition's children to the ring.  wq_out
+    // counts the items not yet finished (dl2's and the ring's): a wave with
+    // nothing to take waits until it is 0 (every wave of the workgroup is
+    // resident, so the waves it waits on make progress) or the block fails.
+    if (t == 0) {
+        L.next_item = 0;
+        L.wq_head = L.wq_tail = L.wq_used = 0;
+        L.wq_out = nitems;
     }
+    for (int k = t; k < (int)kWqRing; k += FT) (&L.q[0][0])[k] = 0;
+    __syncthreads();
+    for (;;) {
+        if (uniform(*(volatile uint32_t*)&L.fail)) break;
+        uint32_t got = 0, lo32 = 0, hi32 = 0;
+        if (lane == 0) {
+            const uint32_t h = *(volatile uint32_t*)&L.wq_head, tl = *(volatile uint32_t*)&L.wq_tail;
+            if (h < tl && atomicCAS(&L.wq_head, h, h + 1) == h) {
+                // claimed ring position h: its item is written right after the
+                // push reserved it
+                volatile uint64_t* slot = &(&L.q[0][0])[h % kWqRing];
+                uint64_t v;
+                while (!((v = *slot) & kWqValid)) __builtin_amdgcn_s_sleep(1);
+                *slot = 0;
+                atomicAdd(&L.wq_used, 1u);
+                lo32 = (uint32_t)v;
+                hi32 = (uint32_t)(v >> 32) & 0x7fffffffu;
+                got = 1;
+            } else if (h >= tl) {
+                const uint32_t k = atomicAdd(&L.next_item, 1u);
+                if (k < nitems) {
+                    const uint64_t v = dl2[k];
+                    lo32 = (uint32_t)v;
+                    hi32 = (uint32_t)(v >> 32);
+                    got = 1;
+                }
+            }
+        }
+        if (!uniform(got)) {
+            if (uniform(*(volatile uint32_t*)&L.wq_out) == 0) break;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const uint64_t it = ((uint64_t)uniform(hi32) << 32) | uniform(lo32);
+        const Seg seg{(uint32_t)it & 0x1ffffu, (uint32_t)(it >> 17) & 0x1ffffu};
+        const uint32_t d = (uint32_t)(it >> 34) & 0xffffu;
+        TBK_T(3, seg.len);
+#ifdef BZ2MI_PHASES
+        const unsigned long long ti0 = wall_clock64();
+#endif
+        if (seg.len <= (uint32_t)kTS) text_sort(Tl, n, sa, seg, d, out, orig, W, L, dl);
+        else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, kWqPush);
+        TBK_T(11, seg.len);
+#ifdef BZ2MI_PHASES
+        TBK_COUNT(seg.len <= (uint32_t)kTS ? 12 : 13, wall_clock64() - ti0);
+#endif
+        if (lane == 0) atomicSub(&L.wq_out, 1u);
+    }
+    __threadfence_block();
+    __syncthreads();
     if (false)
 #endif
     {
@@ -3805,7 +3870,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     }
     __threadfence_block();
     __syncthreads();
-#if BZ2MI_TEXT_DYNDEAL
+#if BZ2MI_TEXT_WQ
     if (false)
 #endif
     {
@@ -3850,7 +3915,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     }
     __threadfence_block();
     __syncthreads();
-    for (int cur = 0;; cur ^= 1) {
+    for (int cur = 0; !BZ2MI_TEXT_WQ; cur ^= 1) {
         // loop conditions from LDS go through readfirstlane: scalar branches
         // (a vector-condition loop around the item calls lost the exec mask)
         const uint32_t nit = uniform(min(L.qn[cur], (uint32_t)kTQ));

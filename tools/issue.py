@@ -15,7 +15,16 @@ Writes profiles/<name>.json, read by bench.py for roofline.issue."""
 import collections
 import csv
 import json
+import os
 import sys
+
+
+def _lib_sha16():
+    """the library the measured command loaded (bench.py refuses a profile of another build)"""
+    import hashlib
+    root = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    path = os.environ.get("BZ2MI_LIBRARY") or os.path.join(root, "bzip2-opencl_amd", "bz2mi", "libbz2mi.so")
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
 
 src = sys.argv[1]
 dst = sys.argv[2]
@@ -45,5 +54,6 @@ for k, c in sorted(acc.items()):
     if c.get("SQ_LDS_IDX_ACTIVE", 0.0) > 0:
         e["lds_bank_conflict_frac"] = round(c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"], 4)
     out["kernels"][k] = e
+out["lib_sha16"] = _lib_sha16()
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out["kernels"], indent=1))

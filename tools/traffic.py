@@ -10,7 +10,16 @@ profiles/<name>.json, read by bench.py for the `traffic` field."""
 import collections
 import csv
 import json
+import os
 import sys
+
+
+def _lib_sha16():
+    """the library the measured command loaded (bench.py refuses a profile of another build)"""
+    import hashlib
+    root = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    path = os.environ.get("BZ2MI_LIBRARY") or os.path.join(root, "bzip2-opencl_amd", "bz2mi", "libbz2mi.so")
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/round"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01_traffic.json"
@@ -27,9 +36,9 @@ for counter, sub, scale in (("FETCH_SIZE", "pmc_fetch", 2.0), ("WRITE_SIZE", "pm
         per[k][key] += float(r["Counter_Value"]) * 1024.0 * scale / steps
         if counter == "FETCH_SIZE":
             per[k]["dispatches"] += 1
-stages = {"front": ["fe_"], "bwt": ["bwt_"], "mtf": ["mtf_kernel"], "huffman": ["huffman_kernel"],
+stages = {"front": ["fe_"], "bwt": ["bwt_", "dbl_"], "mtf": ["mtf_kernel"], "huffman": ["huffman_kernel"],
           "assemble": ["assemble", "offsets_dev", "advance"]}
-out = {"command": "python3 bench.py --no-cpu --no-verify --steps 1 --warmup 1 [--data ...] (1 GiB, -9, p=10)",
+out = {"command": "python3 bench.py --no-cpu --no-verify --steps 1 --warmup 1 " + (sys.argv[5] if len(sys.argv) > 5 else "") + " (1 GiB, -9, p=10)",
        "workload": workload, "note": "bytes per compression of the 1 GiB input; FETCH_SIZE x2 (gfx950 correction)",
        "kernels": {k: {a: round(b) for a, b in v.items()} for k, v in sorted(per.items())},
        "stages": {}}
@@ -37,5 +46,6 @@ for st, pre in stages.items():
     f = sum(v["fetch_bytes"] for k, v in per.items() if any(k.startswith(p) for p in pre))
     w = sum(v["write_bytes"] for k, v in per.items() if any(k.startswith(p) for p in pre))
     out["stages"][st] = {"fetch_bytes": round(f), "write_bytes": round(w), "traffic_bytes": round(f + w)}
+out["lib_sha16"] = _lib_sha16()
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out["stages"], indent=1))
