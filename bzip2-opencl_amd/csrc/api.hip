@@ -1095,6 +1095,7 @@ int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
         case 4: return bz2mi::tbk_stats(out16);
         case 5: return bz2mi::tbk_resolve_stats(out16);
         case 6: return bz2mi::dbl_stats(out16);
+        case 7: return bz2mi::tbk_extra_stats(out16);
         default: return BZ2MI_EINVAL;
     }
 }

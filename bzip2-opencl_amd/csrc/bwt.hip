@@ -32,6 +32,7 @@ namespace bz2mi {
 BZ2MI_PHASE_TABLE(g_bwt_phase)
 BZ2MI_PHASE_TABLE(g_tbk_stat)
 BZ2MI_PHASE_TABLE(g_tbk_res)  // text_resolve sums (PHASES builds)
+BZ2MI_PHASE_TABLE(g_tbk_x)    // text kernel: tie-round and tied-pair wave time (PHASES builds)
 BZ2MI_PHASE_TABLE(g_dbl_stat)  // bwt_finish sums (PHASES builds)
 #ifdef TBK_TRACE
 __device__ unsigned int* g_tbk_trace;
@@ -51,6 +52,15 @@ int tbk_trace(void* p) {
 int tbk_stats(unsigned long long* out) {
 #ifdef BZ2MI_PHASES
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbk_stat), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
+    (void)out;
+    return 0;
+#endif
+}
+
+int tbk_extra_stats(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbk_x), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
 #else
     (void)out;
     return 0;
@@ -3064,7 +3074,13 @@ __device__ TBK_SORT_INL void text_sort_pre(const uint8_t* Tl, int n, uint32_t* s
     TBK_COUNT(7, seg.len);
     uint32_t D = d + kLdsKeyBytes;
     while (tt) {
+#ifdef BZ2MI_PHASES
+        const unsigned long long tp0 = wall_clock64();
+#endif
         tt = uniform(text_pairs(Tl, n, sa, seg.start, tt, D, out, orig, W, L, dl));
+#ifdef BZ2MI_PHASES
+        TBK_COUNT(15, wall_clock64() - tp0);
+#endif
         if (!tt) break;
         TBK_T(8, D << 12 | tt);
         TBK_COUNT(10, 1);
@@ -3087,7 +3103,13 @@ __device__ TBK_SORT_INL void text_sort_pre(const uint8_t* Tl, int n, uint32_t* s
             if (lane == 0) atomicAdd(&L.nflag, tt);
             return;
         }
+#ifdef BZ2MI_PHASES
+        const unsigned long long tr0 = wall_clock64();
+#endif
         tt = uniform(lds_tie_round_upto<kTS / 64>(Tl, n, s, seg.start, tt, D, out, orig, W));
+#ifdef BZ2MI_PHASES
+        TBK_COUNT(14, wall_clock64() - tr0);
+#endif
         D += kLdsTieBytes;
     }
 }
@@ -3221,7 +3243,19 @@ __device__ __forceinline__ int text_cmp_deferred(const uint8_t* Tl, int n, uint3
                                                  uint32_t g, const uint32_t* isa, const uint64_t* dl, uint32_t* link,
                                                  uint32_t* xo) {
     uint32_t p0 = i0 + 1 < (uint32_t)n ? i0 + 1 : 0u, p1 = i1 + 1 < (uint32_t)n ? i1 + 1 : 0u;
+#ifdef BZ2MI_PHASES
+    struct WalkStat {
+        uint32_t x = 0;
+        __device__ ~WalkStat() {
+            atomicAdd(&g_tbk_x[4], (unsigned long long)x);
+            atomicMax(&g_tbk_x[5], (unsigned long long)x);
+        }
+    } ws;
+#endif
     for (uint32_t x = 1; x < (uint32_t)n; ++x) {
+#ifdef BZ2MI_PHASES
+        ws.x = x;
+#endif
         if (x >= d) {
             const uint32_t c0 = Tl[p0], c1 = Tl[p1];
             if (c0 != c1) return c0 < c1 ? -1 : 1;
@@ -3260,7 +3294,19 @@ __device__ __forceinline__ void dg_place(const uint8_t* Tl, int n, uint32_t* sa,
 // -1 (a first), 1, or 0 (equal: periodic)
 __device__ __forceinline__ int text_cmp_plain(const uint8_t* Tl, int n, uint32_t a, uint32_t b, const uint32_t* isa) {
     uint32_t p0 = a, p1 = b;
+#ifdef BZ2MI_PHASES
+    struct WalkStat {
+        uint32_t x = 0;
+        __device__ ~WalkStat() {
+            atomicAdd(&g_tbk_x[2], (unsigned long long)x);
+            atomicMax(&g_tbk_x[3], (unsigned long long)x);
+        }
+    } ws;
+#endif
     for (uint32_t x = 0; x < (uint32_t)n; ++x) {
+#ifdef BZ2MI_PHASES
+        ws.x = x;
+#endif
         const uint32_t c0 = Tl[p0], c1 = Tl[p1];
         if (c0 != c1) return c0 < c1 ? -1 : 1;
         const uint32_t a0 = isa[p0], a1 = isa[p1];
@@ -3328,8 +3374,17 @@ __device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t*
     __syncthreads();
     uint32_t before = 0xffffffffu;
     bool forced = false;  // the previous round ordered the open roots by plain comparison
+#ifdef BZ2MI_PHASES
+    unsigned long long rt0 = 0;
+#endif
     for (uint32_t rr = 0;; ++rr) {
         TBK_T(12, rr << 12 | min(ndef, 4095u));
+#ifdef BZ2MI_PHASES
+        if (rr) {
+            if (t == 0) atomicAdd(&g_tbk_res[6], wall_clock64() - rt0);
+        }
+        rt0 = wall_clock64();
+#endif
 #ifdef BZ2MI_PHASES
         if (t == 0) atomicAdd(&g_tbk_res[3], 1ull);
 #endif
@@ -3391,6 +3446,10 @@ __device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t*
         }
         __threadfence_block();
         __syncthreads();
+#ifdef BZ2MI_PHASES
+        if (t == 0) atomicAdd(&g_tbk_res[1], wall_clock64() - rt0);
+        rt0 = wall_clock64();
+#endif
         // (2) links
         for (int jump = 0; jump < 32; ++jump) {
             TBK_T(13, rr << 8 | (uint32_t)jump);
@@ -3429,6 +3488,10 @@ __device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t*
             __syncthreads();
             if (uniform(L.qn[1]) == 0 || uniform(L.fail)) break;  // nothing placed or jumped
         }
+#ifdef BZ2MI_PHASES
+        if (t == 0) atomicAdd(&g_tbk_res[5], wall_clock64() - rt0);
+        rt0 = wall_clock64();
+#endif
         // (3) larger groups still open: every member against the others
         for (uint32_t gb = (uint32_t)w * 64; gb < ndef; gb += FT) {
             const uint32_t g = gb + (uint32_t)lane;
@@ -3995,6 +4058,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         }
         __threadfence_block();
         __syncthreads();
+#ifdef BZ2MI_PHASES
+        if (t == 0) atomicAdd(&g_tbk_res[0], wall_clock64() - tkr);
+#endif
         text_resolve_all(Tl, n, sa, isa, dl, ndef, dl2, out, orig, L);
         __threadfence_block();
         __syncthreads();
@@ -4157,6 +4223,10 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         }
         atomicMax(&g_tbk_stat[15], wall_clock64() - tk0);
         for (int k = 3; k < 8; ++k) atomicAdd(&g_tbk_stat[k], (unsigned long long)L.stat[k]);
+        atomicAdd(&g_tbk_x[0], (unsigned long long)L.stat[14]);
+        atomicMax(&g_tbk_x[6], tkr);
+        atomicMax(&g_tbk_x[7], tks);
+        atomicAdd(&g_tbk_x[1], (unsigned long long)L.stat[15]);
         for (int k = 10; k < 14; ++k)
             if (k != 11) atomicAdd(&g_tbk_stat[k], (unsigned long long)L.stat[k]);
     }

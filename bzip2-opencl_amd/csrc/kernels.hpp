@@ -166,6 +166,7 @@ int bwt_phases(unsigned long long* out);
 int mtf_phases(unsigned long long* out);
 int fe_phases(unsigned long long* out);
 int tbk_stats(unsigned long long* out);
+int tbk_extra_stats(unsigned long long* out);
 int tbk_resolve_stats(unsigned long long* out);
 int dbl_stats(unsigned long long* out);
 int tbk_trace(void* host_mapped);

@@ -41,4 +41,11 @@ print(f"  deferred: {r[8]} blocks with deferred groups, {r[2] / nr:.0f} groups p
       f"partition depth {r[15]}")
 print(f"  resolve work per deferring block: rounds {r[3] / nr:.1f}, jump iterations {r[4] / nr:.1f}, plain-comparison "
       f"passes {r[7]} in all")
+print(f"  resolve time per deferring block (thread 0): isa/marks {r[0] / nr / 100:.1f} us, pairs+groups "
+      f"{r[1] / nr / 100:.1f}, links {r[5] / nr / 100:.1f}, step 3 + count (rounds before the last) {r[6] / nr / 100:.1f}")
+print("rc", L.bz2mi_debug_phases(7, buf))
+x = list(buf)
+print(f"  wave time per block: tie rounds {x[0] / nb / 100:.1f} us, tied pairs {x[1] / nb / 100:.1f} us")
+print(f"  walks: plain comparisons {x[2]} steps in all (longest {x[3]}), deferred comparisons {x[4]} steps (longest "
+      f"{x[5]}); slowest resolve {x[6] / 100:.1f} us, slowest sort phase {x[7] / 100:.1f} us")
 print("timings", ctx.timings())
