@@ -2964,15 +2964,28 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
     uint32_t nkeep = 0, nfl = 0;
     bool dwant[E];
     uint32_t dst_[E], ddep[E];
+    // items are blocked (item lane * E + e in element e): the neighbours
+    // q - 1, q + 1, q + 2 are the lane's own elements or the adjacent lanes'
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t q = (uint32_t)(lane * E + e);
         wv[e] = q < tt ? W[q] : 0u;
+    }
+    uint32_t nxt[2];  // the next lane's elements 0 and 1
+    nxt[0] = (uint32_t)__shfl_down((int)wv[0], 1);
+    nxt[1] = E > 1 ? (uint32_t)__shfl_down((int)wv[E > 1 ? 1 : 0], 1) : 0u;
+    const uint32_t prv = lane_prev(wv[E - 1], 0u);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t q = (uint32_t)(lane * E + e);
+        const uint32_t w1 = e + 1 < E ? wv[e + 1 < E ? e + 1 : 0] : nxt[0];
+        const uint32_t w2 = e + 2 < E ? wv[e + 2 < E ? e + 2 : 0] : nxt[e + 2 - E < 2 ? e + 2 - E : 0];
+        const uint32_t wm = e > 0 ? wv[e > 0 ? e - 1 : 0] : prv;
         const bool h0 = q < tt && (wv[e] >> 26);
-        const bool h1 = q + 1 < tt && (W[q + 1] >> 26);
-        const bool h2 = q + 2 >= tt || (W[q + 2] >> 26);
+        const bool h1 = q + 1 < tt && (w1 >> 26);
+        const bool h2 = q + 2 >= tt || (w2 >> 26);
         ph[e] = h0 && q + 1 < tt && !h1 && h2;  // the head of a group of two
-        const bool hm = q >= 1 && (W[q - 1] >> 26) && !h0 && (q + 1 >= tt || h1);  // its second item
+        const bool hm = q >= 1 && (wm >> 26) && !h0 && (q + 1 >= tt || h1);  // its second item
         keep[e] = q < tt && !ph[e] && !hm;
         nkeep += keep[e] ? 1u : 0u;
     }
@@ -2983,8 +2996,7 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
         dst_[e] = 0;
         ddep[e] = 0;
         if (!ph[e]) continue;
-        const uint32_t q = (uint32_t)(lane * E + e);
-        const uint32_t w1 = W[q + 1];
+        const uint32_t w1 = e + 1 < E ? wv[e + 1 < E ? e + 1 : 0] : nxt[0];
         const uint32_t i0 = wv[e] & 0x1ffffu, i1 = w1 & 0x1ffffu;
         const uint32_t s0 = (wv[e] >> 17) & 511u, s1 = (w1 >> 17) & 511u;
         const uint32_t lo = min(s0, s1);
@@ -3291,7 +3303,11 @@ __device__ __forceinline__ void dg_place(const uint8_t* Tl, int n, uint32_t* sa,
 
 // Order of rotations a != b from their first byte on, by bytes and known
 // positions only (deferred and not yet copied rotations are walked over):
-// -1 (a first), 1, or 0 (equal: periodic)
+// -1 (a first), 1, or 0 (equal: periodic).  Eight bytes at a time from the
+// LDS text; the known positions (global isa) only once per 64 bytes -- any x
+// up to which the rotations agree and where both a + x and b + x are placed
+// decides the same way as the first differing byte, so the checks only end
+// the walk early (a walk through a long repeat is bytes, not isa loads).
 __device__ __forceinline__ int text_cmp_plain(const uint8_t* Tl, int n, uint32_t a, uint32_t b, const uint32_t* isa) {
     uint32_t p0 = a, p1 = b;
 #ifdef BZ2MI_PHASES
@@ -3303,16 +3319,20 @@ __device__ __forceinline__ int text_cmp_plain(const uint8_t* Tl, int n, uint32_t
         }
     } ws;
 #endif
-    for (uint32_t x = 0; x < (uint32_t)n; ++x) {
+    for (uint32_t x = 0; x < (uint32_t)n + 8; x += 8) {
 #ifdef BZ2MI_PHASES
         ws.x = x;
 #endif
-        const uint32_t c0 = Tl[p0], c1 = Tl[p1];
-        if (c0 != c1) return c0 < c1 ? -1 : 1;
-        const uint32_t a0 = isa[p0], a1 = isa[p1];
-        if (a0 < kDefMark && a1 < kDefMark) return a0 < a1 ? -1 : 1;
-        if (++p0 == (uint32_t)n) p0 = 0;
-        if (++p1 == (uint32_t)n) p1 = 0;
+        if ((x & 63u) == 0 && x) {
+            const uint32_t a0 = isa[p0], a1 = isa[p1];
+            if (a0 < kDefMark && a1 < kDefMark) return a0 < a1 ? -1 : 1;
+        }
+        const uint64_t w0 = load8(Tl, n, p0), w1 = load8(Tl, n, p1);
+        if (w0 != w1) return w0 < w1 ? -1 : 1;
+        p0 += 8;
+        p1 += 8;
+        if (p0 >= (uint32_t)n) p0 -= (uint32_t)n;
+        if (p1 >= (uint32_t)n) p1 -= (uint32_t)n;
     }
     return 0;
 }
@@ -4044,11 +4064,25 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     unsigned long long tkr = wall_clock64();
 #endif
     if (ndef != 0 && !uniform(L.fail)) {
-        for (uint32_t k = t; k < (uint32_t)n; k += FT) {
-            const uint32_t v = ld_fresh(sa + k), i = v & 0x1ffffu;
-            const uint32_t rx = L.rank[Tl[i]], rc = L.rank[Tl[i + 1 < (uint32_t)n ? i + 1 : 0u]];
-            const bool implicit = rx >= s_big && rc < rx;
-            isa[i] = (implicit || (v & kUnres)) ? kNoIsa : k;
+        // 8 SA entries per thread in flight, then their (scattered) isa stores
+        constexpr int U = 8;
+        for (uint32_t k0 = t; k0 < (uint32_t)n; k0 += FT * U) {
+            uint32_t v[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const uint32_t k = k0 + (uint32_t)j * FT;
+                v[j] = k < (uint32_t)n ? ld_fresh(sa + k) : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const uint32_t k = k0 + (uint32_t)j * FT;
+                if (k < (uint32_t)n) {
+                    const uint32_t i = v[j] & 0x1ffffu;
+                    const uint32_t rx = L.rank[Tl[i]], rc = L.rank[Tl[i + 1 < (uint32_t)n ? i + 1 : 0u]];
+                    const bool implicit = rx >= s_big && rc < rx;
+                    isa[i] = (implicit || (v[j] & kUnres)) ? kNoIsa : k;
+                }
+            }
         }
         __threadfence_block();
         __syncthreads();

@@ -47,8 +47,12 @@ def _input(src: str) -> bytes:
     if kind == "pins":
         return make_pins.make_input(name)
     from bz2mi import synth
-    assert src == "synth.random_bytes(1<<20, 0x5EED2001)"
-    return synth.random_bytes(1 << 20, 0x5EED2001).tobytes()
+    if src == "synth.random_bytes(1<<20, 0x5EED2001)":
+        return synth.random_bytes(1 << 20, 0x5EED2001).tobytes()
+    # round 5 (tools/ref_opencl3.sh): "synth:<generator>:<bytes>[:<seed>]"
+    _, gen, nbytes, *seed = src.split(":")
+    fn = {"repeats": synth.repeats_bytes, "realtext": synth.realtext_bytes}[gen]
+    return (fn(int(nbytes), int(seed[0], 0)) if seed else fn(int(nbytes))).tobytes()
 
 
 def _ids(e):
