@@ -2962,8 +2962,6 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
     uint32_t wv[E];
     bool keep[E], ph[E];
     uint32_t nkeep = 0, nfl = 0;
-    bool dwant[E];
-    uint32_t dst_[E], ddep[E];
     // items are blocked (item lane * E + e in element e): the neighbours
     // q - 1, q + 1, q + 2 are the lane's own elements or the adjacent lanes'
 #pragma unroll
@@ -2989,48 +2987,68 @@ __device__ __forceinline__ uint32_t text_pairs(const uint8_t* Tl, int n, uint32_
         keep[e] = q < tt && !ph[e] && !hm;
         nkeep += keep[e] ? 1u : 0u;
     }
-    __builtin_amdgcn_wave_barrier();
+    // the pair heads' (first, second) items compacted to W[256, 256 + 2 np):
+    // the comparisons then run one pair per lane, in one divergent pass
+    uint32_t* PW = W + 256;
+    uint32_t myp = 0;
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        dwant[e] = false;
-        dst_[e] = 0;
-        ddep[e] = 0;
-        if (!ph[e]) continue;
-        const uint32_t w1 = e + 1 < E ? wv[e + 1 < E ? e + 1 : 0] : nxt[0];
-        const uint32_t i0 = wv[e] & 0x1ffffu, i1 = w1 & 0x1ffffu;
-        const uint32_t s0 = (wv[e] >> 17) & 511u, s1 = (w1 >> 17) & 511u;
-        const uint32_t lo = min(s0, s1);
-        uint32_t p0 = (i0 + D) % (uint32_t)n, p1 = (i1 + D) % (uint32_t)n;
-        int cmp = 0;
-        uint32_t dd = D;
-        for (; dd < (uint32_t)kTextPairCap; dd += 8) {
-            const uint64_t x0 = load8(Tl, n, p0), x1 = load8(Tl, n, p1);
-            if (x0 != x1) {
-                cmp = x0 < x1 ? -1 : 1;
-                break;
+    for (int e = 0; e < E; ++e) myp += ph[e] ? 1u : 0u;
+    const uint32_t pinc = wave_incl_sum(myp);
+    const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)pinc, 63);
+    if (np) {
+        uint32_t j = pinc - myp;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (ph[e]) {
+                PW[2 * j] = wv[e];
+                PW[2 * j + 1] = e + 1 < E ? wv[e + 1 < E ? e + 1 : 0] : nxt[0];
+                ++j;
             }
-            p0 += 8;
-            p1 += 8;
-            if (p0 >= (uint32_t)n) p0 -= (uint32_t)n;
-            if (p1 >= (uint32_t)n) p1 -= (uint32_t)n;
-        }
-        if (cmp) {
-            const uint32_t a = cmp < 0 ? i0 : i1, c = cmp < 0 ? i1 : i0;
-            sa[base + lo] = a;
-            sa[base + lo + 1] = c;
-            text_final(Tl, n, base + lo, a, out, orig);
-            text_final(Tl, n, base + lo + 1, c, out, orig);
-        } else {  // deferred: a group of two sharing dd bytes
-            sa[base + lo] = i0 | kUnres;
-            sa[base + lo + 1] = i1 | kUnres;
-            nfl += 2;
-            dwant[e] = true;
-            dst_[e] = base + lo;
-            ddep[e] = dd;
         }
     }
-#pragma unroll
-    for (int e = 0; e < E; ++e) dg_push(L, dl, dwant[e], dst_[e], 2, ddep[e]);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t k0 = 0; k0 < np; k0 += 64) {
+        const uint32_t k = k0 + (uint32_t)lane;
+        bool dwant = false;
+        uint32_t dst = 0, ddep = 0;
+        if (k < np) {
+            const uint32_t w0 = PW[2 * k], w1 = PW[2 * k + 1];
+            const uint32_t i0 = w0 & 0x1ffffu, i1 = w1 & 0x1ffffu;
+            const uint32_t s0 = (w0 >> 17) & 511u, s1 = (w1 >> 17) & 511u;
+            const uint32_t lo = min(s0, s1);
+            uint32_t p0 = i0 + D, p1 = i1 + D;
+            if (p0 >= (uint32_t)n) p0 %= (uint32_t)n;
+            if (p1 >= (uint32_t)n) p1 %= (uint32_t)n;
+            int cmp = 0;
+            uint32_t dd = D;
+            for (; dd < (uint32_t)kTextPairCap; dd += 8) {
+                const uint64_t x0 = load8(Tl, n, p0), x1 = load8(Tl, n, p1);
+                if (x0 != x1) {
+                    cmp = x0 < x1 ? -1 : 1;
+                    break;
+                }
+                p0 += 8;
+                p1 += 8;
+                if (p0 >= (uint32_t)n) p0 -= (uint32_t)n;
+                if (p1 >= (uint32_t)n) p1 -= (uint32_t)n;
+            }
+            if (cmp) {
+                const uint32_t a = cmp < 0 ? i0 : i1, c = cmp < 0 ? i1 : i0;
+                sa[base + lo] = a;
+                sa[base + lo + 1] = c;
+                text_final(Tl, n, base + lo, a, out, orig);
+                text_final(Tl, n, base + lo + 1, c, out, orig);
+            } else {  // deferred: a group of two sharing dd bytes
+                sa[base + lo] = i0 | kUnres;
+                sa[base + lo + 1] = i1 | kUnres;
+                nfl += 2;
+                dwant = true;
+                dst = base + lo;
+                ddep = dd;
+            }
+        }
+        dg_push(L, dl, dwant, dst, 2, ddep);
+    }
     const uint32_t nf = wave_sum(nfl);
     if (nf && lane == 0) atomicAdd(&L.nflag, nf);
     const uint32_t inc = wave_incl_sum(nkeep);
@@ -3734,6 +3752,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         atomicOr(&L.mask[a][c2 >> 5], 1u << (c2 & 31u));
     }
     __syncthreads();
+#ifdef BZ2MI_PHASES
+    if (t == 0) atomicAdd(&g_tbk_x[8], wall_clock64() - tk0);
+#endif
     uint32_t P;
     {
         const uint32_t q0 = (uint32_t)t * 2;  // (first byte, word) = (q >> 3, q & 7)
@@ -3758,6 +3779,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     };
     for (int i = t; i < n; i += FT) atomicAdd(&cnt[pair_of(Tl[i], Tl[i + 1 < n ? i + 1 : 0])], 1u);
     __syncthreads();
+#ifdef BZ2MI_PHASES
+    if (t == 0) atomicAdd(&g_tbk_x[9], wall_clock64() - tk0);
+#endif
     {
         // pair starts in place (each thread a contiguous run of pairs)
         const uint32_t per = (P + FT - 1) / FT;
@@ -3794,6 +3818,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     const uint32_t K = (uint32_t)__syncthreads_count(t < 256 && L.cstart[t + 1] > L.cstart[t]);
     const uint32_t s0 = 256u - K;
     const uint32_t s_big = max(s0, 256u - (uint32_t)kCopySteps);
+#ifdef BZ2MI_PHASES
+    if (t == 0) atomicAdd(&g_tbk_x[10], wall_clock64() - tk0);
+#endif
     // the pair list (global): start, length, bytes, sorted-explicitly flag
     for (uint32_t q = t; q < 2048; q += FT) {
         const uint32_t a = q >> 3, wq = q & 7u;
@@ -3808,6 +3835,9 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         }
     }
     __syncthreads();
+#ifdef BZ2MI_PHASES
+    if (t == 0) atomicAdd(&g_tbk_x[11], wall_clock64() - tk0);
+#endif
     // ---- every rotation to its pair bucket
     for (int i = t; i < n; i += FT)
         sa[atomicAdd(&cnt[pair_of(Tl[i], Tl[i + 1 < n ? i + 1 : 0])], 1u)] = (uint32_t)i;
@@ -4064,7 +4094,17 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     unsigned long long tkr = wall_clock64();
 #endif
     if (ndef != 0 && !uniform(L.fail)) {
-        // 8 SA entries per thread in flight, then their (scattered) isa stores
+        // kNoIsa everywhere (coalesced), then the positions of the placed
+        // rotations (scattered stores for about half of them: the copy
+        // targets and the deferred members keep kNoIsa), 8 SA entries per
+        // thread in flight
+        {
+            uint4* I4 = reinterpret_cast<uint4*>(isa);
+            const uint4 none = make_uint4(kNoIsa, kNoIsa, kNoIsa, kNoIsa);
+            for (uint32_t k = t; k < ((uint32_t)n + 3) / 4; k += FT) I4[k] = none;
+        }
+        __threadfence_block();
+        __syncthreads();
         constexpr int U = 8;
         for (uint32_t k0 = t; k0 < (uint32_t)n; k0 += FT * U) {
             uint32_t v[U];
@@ -4080,7 +4120,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                     const uint32_t i = v[j] & 0x1ffffu;
                     const uint32_t rx = L.rank[Tl[i]], rc = L.rank[Tl[i + 1 < (uint32_t)n ? i + 1 : 0u]];
                     const bool implicit = rx >= s_big && rc < rx;
-                    isa[i] = (implicit || (v[j] & kUnres)) ? kNoIsa : k;
+                    if (!implicit && !(v[j] & kUnres)) isa[i] = k;
                 }
             }
         }

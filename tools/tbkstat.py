@@ -48,4 +48,6 @@ x = list(buf)
 print(f"  wave time per block: tie rounds {x[0] / nb / 100:.1f} us, tied pairs {x[1] / nb / 100:.1f} us")
 print(f"  walks: plain comparisons {x[2]} steps in all (longest {x[3]}), deferred comparisons {x[4]} steps (longest "
       f"{x[5]}); slowest resolve {x[6] / 100:.1f} us, slowest sort phase {x[7] / 100:.1f} us")
+print(f"  setup to (thread 0, cumulative per block): text+mask {x[8] / nb / 100:.1f} us, pair counts {x[9] / nb / 100:.1f}, "
+      f"starts+order {x[10] / nb / 100:.1f}, pair list {x[11] / nb / 100:.1f}, scatter = setup total")
 print("timings", ctx.timings())
