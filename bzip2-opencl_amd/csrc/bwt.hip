@@ -976,6 +976,11 @@ __device__ __forceinline__ uint64_t lds_key(const uint8_t* __restrict__ T, int n
 // prefix doubling) with their SA entries written.  Requires n < 2^17.
 constexpr int kLdsKeyBytes = 6;   // bytes of the first round
 constexpr int kLdsTieBytes = 5;   // bytes of every tie round
+// the same for IB item-index bits (9: up to 512 items; 8: up to 256, one more
+// text byte per round)
+__host__ __device__ constexpr int lds_key_bytes(int IB) { return (64 - IB) / 8; }
+__host__ __device__ constexpr int lds_tie_bytes(int IB) { return (64 - 2 * IB) / 8; }
+static_assert(lds_key_bytes(9) == kLdsKeyBytes && lds_tie_bytes(9) == kLdsTieBytes, "LDS key layout");
 
 __device__ __forceinline__ uint64_t lane_next64(uint64_t v) {
     const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1), hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1);
@@ -987,7 +992,7 @@ __device__ __forceinline__ uint64_t lane_prev64(uint64_t v) {
 
 // one emission pass over sorted unique keys (prefix = key >> 9): final items
 // are written, tied ones compacted into idx[0, t) for the next round; returns t
-template <int E>
+template <int E, int IB = 9>
 __device__ __forceinline__ uint32_t lds_emit_round(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t base,
                                                    uint32_t m, const uint64_t (&key)[E], const uint32_t (&src)[E],
                                                    const uint32_t (&dst)[E], uint8_t* __restrict__ bwt,
@@ -995,7 +1000,7 @@ __device__ __forceinline__ uint32_t lds_emit_round(const uint8_t* __restrict__ T
     const int lane = lane_id();
     uint64_t pk[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) pk[e] = key[e] >> 9;
+    for (int e = 0; e < E; ++e) pk[e] = key[e] >> IB;
     const uint64_t before = lane_prev64(pk[E - 1]), after = lane_next64(pk[0]);
     bool tie[E], head[E];
     uint32_t cnt = 0;
@@ -1029,7 +1034,7 @@ __device__ __forceinline__ uint32_t lds_emit_round(const uint8_t* __restrict__ T
 }
 
 // tie round over the t compacted items idx[0, t) at depth D
-template <int E>
+template <int E, int IB = 9>
 __device__ __forceinline__ uint32_t lds_tie_round(const uint8_t* __restrict__ T, int n, Scratch& s, uint32_t base,
                                                uint32_t t, uint32_t D, uint8_t* __restrict__ bwt,
                                                uint32_t* __restrict__ orig, uint32_t* __restrict__ idx) {
@@ -1051,7 +1056,7 @@ __device__ __forceinline__ uint32_t lds_tie_round(const uint8_t* __restrict__ T,
         if (q < t) {
             const uint32_t g = gs[e] > carry ? gs[e] : carry;
             const uint32_t p = (uint32_t)(((uint64_t)key[e] + D) % (uint32_t)n);
-            key[e] = ((uint64_t)g << 49) | ((load8(T, n, p) >> 24) << 9) | q;
+            key[e] = ((uint64_t)g << (IB + 8 * lds_tie_bytes(IB))) | ((load8(T, n, p) >> (64 - 8 * lds_tie_bytes(IB))) << IB) | q;
         }
     }
     uint32_t dummy[E];
@@ -1060,10 +1065,10 @@ __device__ __forceinline__ uint32_t lds_tie_round(const uint8_t* __restrict__ T,
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t r = (uint32_t)(lane * E + e);
-        src[e] = r < t ? idx[key[e] & 511u] & 0x1ffffu : 0u;
+        src[e] = r < t ? idx[key[e] & ((1u << IB) - 1u)] & 0x1ffffu : 0u;
         dst[e] = r < t ? (idx[r] >> 17) & 511u : 0u;
     }
-    return lds_emit_round<E>(T, n, s, base, t, key, src, dst, bwt, orig, idx);
+    return lds_emit_round<E, IB>(T, n, s, base, t, key, src, dst, bwt, orig, idx);
 }
 
 __device__ __forceinline__ uint32_t lds_tie_round_any(const uint8_t* T, int n, Scratch& s, uint32_t base, uint32_t t,
@@ -1075,13 +1080,13 @@ __device__ __forceinline__ uint32_t lds_tie_round_any(const uint8_t* T, int n, S
 }
 
 // the same for at most 64 * MAXE items (no instance of the larger rounds)
-template <int MAXE>
+template <int MAXE, int IB = 9>
 __device__ __forceinline__ uint32_t lds_tie_round_upto(const uint8_t* T, int n, Scratch& s, uint32_t base, uint32_t t,
                                                        uint32_t D, uint8_t* bwt, uint32_t* orig, uint32_t* idx) {
-    if (t <= 64) return lds_tie_round<1>(T, n, s, base, t, D, bwt, orig, idx);
-    if (MAXE <= 2 || t <= 128) return lds_tie_round<MAXE <= 2 ? MAXE : 2>(T, n, s, base, t, D, bwt, orig, idx);
-    if (MAXE <= 4 || t <= 256) return lds_tie_round<MAXE <= 4 ? MAXE : 4>(T, n, s, base, t, D, bwt, orig, idx);
-    return lds_tie_round<MAXE>(T, n, s, base, t, D, bwt, orig, idx);
+    if (t <= 64) return lds_tie_round<1, IB>(T, n, s, base, t, D, bwt, orig, idx);
+    if (MAXE <= 2 || t <= 128) return lds_tie_round<MAXE <= 2 ? MAXE : 2, IB>(T, n, s, base, t, D, bwt, orig, idx);
+    if (MAXE <= 4 || t <= 256) return lds_tie_round<MAXE <= 4 ? MAXE : 4, IB>(T, n, s, base, t, D, bwt, orig, idx);
+    return lds_tie_round<MAXE, IB>(T, n, s, base, t, D, bwt, orig, idx);
 }
 
 // groups still tied at the depth limit: SA entries written, groups to the sink
@@ -1139,7 +1144,7 @@ __device__ __forceinline__ uint32_t wave_sort_lds_text(const uint8_t* __restrict
 // sorted into LDS sub-buckets first and its keys are gathered from the text
 // once.  (Any placement of unsorted items over the slots is a valid input of
 // the bitonic network.)
-template <int ES, int PE>
+template <int ES, int PE, int IB = 9>
 __device__ __forceinline__ uint32_t wave_sort_pre_text(const uint8_t* __restrict__ T, int n, Scratch& s,
                                                        uint32_t start, uint32_t m, uint32_t d,
                                                        uint8_t* __restrict__ bwt, uint32_t* __restrict__ orig,
@@ -1156,7 +1161,7 @@ __device__ __forceinline__ uint32_t wave_sort_pre_text(const uint8_t* __restrict
             idx[g] = i;
             uint32_t p = i + d;
             if (p >= (uint32_t)n) p %= (uint32_t)n;
-            key[e] = ((load8(T, n, p) >> (64 - 8 * kLdsKeyBytes)) << 9) | g;
+            key[e] = ((load8(T, n, p) >> (64 - 8 * lds_key_bytes(IB))) << IB) | g;
         } else {
             key[e] = ~0ull;
         }
@@ -1168,10 +1173,10 @@ __device__ __forceinline__ uint32_t wave_sort_pre_text(const uint8_t* __restrict
 #pragma unroll
     for (int e = 0; e < ES; ++e) {
         const uint32_t r = (uint32_t)(lane * ES + e);
-        src[e] = r < m ? idx[key[e] & 511u] : 0u;
+        src[e] = r < m ? idx[key[e] & ((1u << IB) - 1u)] : 0u;
         dst[e] = r;
     }
-    return lds_emit_round<ES>(T, n, s, start, m, key, src, dst, bwt, orig, idx);
+    return lds_emit_round<ES, IB>(T, n, s, start, m, key, src, dst, bwt, orig, idx);
 }
 
 // the tie rounds after a first round left t items tied (depth d + kLdsKeyBytes)
@@ -2729,6 +2734,7 @@ constexpr int kTextPairCap = BZ2MI_TEXT_PAIRCAP;  // depth to which two tied rot
 #define BZ2MI_TEXT_SMALL 256
 #endif
 constexpr int kTS = BZ2MI_TEXT_SMALL;
+constexpr int kTIB = kTS == 256 ? 8 : 9;  // item-index bits of its sort keys (7 text bytes in the first round, 6 per tie round)
 static_assert(kTS == 256 || kTS == 512, "text sort size");
 constexpr int kTQ = 512;          // work items per round
 constexpr int kCopyR = 4;         // rotations per lane and chunk of a copy step
@@ -3095,14 +3101,14 @@ __device__ TBK_SORT_INL void text_sort_pre(const uint8_t* Tl, int n, uint32_t* s
     Scratch s{};
     s.sa = sa;
     uint32_t tt;
-    if (seg.len <= 64) tt = wave_sort_pre_text<1>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
-    else if (seg.len <= 128) tt = wave_sort_pre_text<2>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
-    else if (kTS <= 256 || seg.len <= 256) tt = wave_sort_pre_text<kTS <= 256 ? kTS / 64 : 4>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
-    else tt = wave_sort_pre_text<kTS / 64>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    if (seg.len <= 64) tt = wave_sort_pre_text<1, kTS / 64, kTIB>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    else if (seg.len <= 128) tt = wave_sort_pre_text<2, kTS / 64, kTIB>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    else if (kTS <= 256 || seg.len <= 256) tt = wave_sort_pre_text<kTS <= 256 ? kTS / 64 : 4, kTS / 64, kTIB>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
+    else tt = wave_sort_pre_text<kTS / 64, kTS / 64, kTIB>(Tl, n, s, seg.start, seg.len, d, out, orig, W, pre);
     tt = uniform(tt);
     TBK_COUNT(4, 1);
     TBK_COUNT(7, seg.len);
-    uint32_t D = d + kLdsKeyBytes;
+    uint32_t D = d + lds_key_bytes(kTIB);
     while (tt) {
 #ifdef BZ2MI_PHASES
         const unsigned long long tp0 = wall_clock64();
@@ -3114,7 +3120,7 @@ __device__ TBK_SORT_INL void text_sort_pre(const uint8_t* Tl, int n, uint32_t* s
         if (!tt) break;
         TBK_T(8, D << 12 | tt);
         TBK_COUNT(10, 1);
-        if (D + kLdsTieBytes > (uint32_t)kTextTieCap) {
+        if (D + lds_tie_bytes(kTIB) > (uint32_t)kTextTieCap) {
             // deferred: the tied items keep their slots, flagged; every group
             // (a head item and the items up to the next head, consecutive
             // slots from the head's) to the deferred list
@@ -3136,11 +3142,11 @@ __device__ TBK_SORT_INL void text_sort_pre(const uint8_t* Tl, int n, uint32_t* s
 #ifdef BZ2MI_PHASES
         const unsigned long long tr0 = wall_clock64();
 #endif
-        tt = uniform(lds_tie_round_upto<kTS / 64>(Tl, n, s, seg.start, tt, D, out, orig, W));
+        tt = uniform(lds_tie_round_upto<kTS / 64, kTIB>(Tl, n, s, seg.start, tt, D, out, orig, W));
 #ifdef BZ2MI_PHASES
         TBK_COUNT(14, wall_clock64() - tr0);
 #endif
-        D += kLdsTieBytes;
+        D += lds_tie_bytes(kTIB);
     }
 }
 
