@@ -100,8 +100,18 @@ int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks) {
 int stage_front(bz2mi_ctx* c, Batch& t, const FrontBufs& f, const uint8_t* d_x, size_t n, uint64_t first,
                 uint64_t cnt, hipStream_t s) {
     using namespace bz2mi;
-    hipLaunchKernelGGL(fe_rle1_kernel, dim3((unsigned)cnt), dim3(256), 0, s, d_x, (uint64_t)n, f.d_starts, first,
-                       cnt, t.d_blocks, c->stride, t.d_lens, t.d_crc, c->d_crctab);
+    // the batch's segments, their emission counts (cut blocks only), the
+    // emission, then the CRCs of the cut blocks; grid: every block plus one
+    // workgroup per kFeSegLen bytes of the input (a bound on the extra segments)
+    auto* seg = reinterpret_cast<const FeSeg*>(f.d_seg);
+    hipLaunchKernelGGL(fe_segplan_kernel, dim3(1), dim3(1024), 0, s, d_x, (uint64_t)n, f.d_starts, first, cnt, f.d_rsb,
+                       f.d_summ,                       reinterpret_cast<FeSeg*>(f.d_seg), f.d_segfirst, (uint64_t)f.seg_cap, f.d_nseg);
+    const unsigned grid = (unsigned)std::min<uint64_t>(f.seg_cap, cnt + n / kFeSegLen + 1);
+    for (int mode = 0; mode < 2; ++mode)
+        hipLaunchKernelGGL(fe_rle1_kernel, dim3(grid), dim3(256), 0, s, d_x, (uint64_t)n, seg, f.d_segfirst, f.d_nseg,
+                           f.d_segcnt, f.d_segcrc, mode, t.d_blocks, c->stride, t.d_lens, t.d_crc, c->d_crctab);
+    hipLaunchKernelGGL(fe_crccomb_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, seg, f.d_segfirst, cnt,
+                       f.d_segcrc, t.d_crc, c->d_crctab);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("front-rle1");
     return BZ2MI_OK;
@@ -393,6 +403,14 @@ int ensure_front(FrontBufs& f, int S, size_t n) {
     if ((r = dalloc(&f.d_bnd, maxb + 2))) return r;
     if ((r = dalloc(&f.d_starts, maxb + 3))) return r;
     if ((r = dalloc(&f.d_nb, 4))) return r;
+    // segments: one per block, plus one per kFeSegLen raw bytes of a cut block
+    const size_t segs = maxb + cap / bz2mi::kFeSegLen + 8;
+    if ((r = dalloc(&f.d_seg, segs * bz2mi::kFeSegBytes))) return r;
+    if ((r = dalloc(&f.d_segfirst, maxb + 8))) return r;
+    if ((r = dalloc(&f.d_nseg, 4))) return r;
+    if ((r = dalloc(&f.d_segcnt, segs))) return r;
+    if ((r = dalloc(&f.d_segcrc, segs))) return r;
+    f.seg_cap = segs;
     f.n_cap = cap;
     f.maxb = maxb;
     return BZ2MI_OK;

@@ -1040,31 +1040,35 @@ __device__ __forceinline__ uint32_t crc_map(const uint32_t* __restrict__ T, uint
     return T[x & 255u] ^ T[256 + ((x >> 8) & 255u)] ^ T[512 + ((x >> 16) & 255u)] ^ T[768 + (x >> 24)];
 }
 
-__global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict__ x, uint64_t n,
-                                                      const uint64_t* __restrict__ starts, uint64_t first, uint64_t count,
-                                                      uint8_t* __restrict__ blocks, size_t stride,
-                                                      uint32_t* __restrict__ lens, uint32_t* __restrict__ crcs,
-                                                      const uint32_t* __restrict__ crc_tabs) {
-    __shared__ uint4 tin4[2 * kTile / 16 + 4];
-    __shared__ uint8_t tout[kTileOut];
-    __shared__ uint32_t tmp[8];
-    __shared__ uint32_t lastv[256];
-    __shared__ uint32_t tslice[1024], t4096[1024];
-    const uint64_t lb = blockIdx.x;  // batch-local block
-    if (lb >= count) return;
-    const uint64_t b = first + lb;
+// Long raw blocks (run-heavy input: a block can cover 4.6 MB) are cut into
+// segments of about kFeSegLen bytes, each emitted by a workgroup of its own.
+// A cut is clean -- a run start, or a 255-byte piece boundary inside a run
+// (the block-local run phase there is 0) -- so every segment is an RLE1
+// encoding of its own: the emission restarts the piece phase at the cut
+// exactly as the sequential encoder does there.  Segment output offsets are
+// the emission counts of the earlier segments (a counting pass), and segment
+// CRCs combine as crc(A|B) = A_{|B|}(crc(A)) ^ crc(B) on raw registers.
+struct FeSeg {
+    uint64_t lo, hi;  // input bytes [lo, hi)
+    uint32_t lb, s;   // batch-local block, segment index within the block
+};
+static_assert(sizeof(FeSeg) == kFeSegBytes, "segment table entry");
+
+// Emission (mode 1) or only its byte count (mode 0) of input bytes [lo, hi)
+// that start a piece, into out[o0, ...): returns the count.  CRC (mode 1):
+// the raw register (from 0) of [lo, hi) in *raw.
+template <int MODE>
+__device__ uint32_t rle1_range(const uint8_t* __restrict__ x, uint64_t n, uint64_t lo_, uint64_t hi_,
+                               uint8_t* __restrict__ out, uint32_t o0, uint32_t* raw,
+                               const uint32_t* __restrict__ tslice, const uint32_t* __restrict__ t4096,
+                               const uint32_t* __restrict__ crc_tabs, uint4* tin4, uint8_t* tout, uint32_t* tmp,
+                               uint32_t* lastv) {
     const int t = threadIdx.x;
-    const uint64_t p0 = starts[b], p1 = starts[b + 1];
-    uint8_t* out = blocks + lb * stride;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        tslice[t + 256 * k] = crc_tabs[t + 256 * k];
-        t4096[t + 256 * k] = crc_tabs[kCrcShiftBase + 1024 * 12 + t + 256 * k];
-    }
+    const uint64_t p0 = lo_, p1 = hi_;
     const uint64_t pad = (kTile - (p1 - p0) % kTile) % kTile;
     uint32_t acc = 0;
     const uint8_t* tin = reinterpret_cast<const uint8_t*>(tin4);
-    uint32_t o_carry = 0;
+    uint32_t o_carry = o0;
     uint64_t rs_carry = p0;  // run start in effect before the tile
     for (uint64_t base = p0; base < p1; base += kTile) {
         // stage [abase, abase + 16*nvec) covering base-1 .. base+kTile and the
@@ -1087,7 +1091,7 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         }
         __syncthreads();
         const uint32_t off0 = (uint32_t)(base - abase);
-        {  // CRC of padded-tile bytes [16t, 16t+16): real positions base - pad + 16t + k
+        if (MODE == 1) {  // CRC of padded-tile bytes [16t, 16t+16): real positions base - pad + 16t + k
             const int64_t r0 = (int64_t)base - (int64_t)pad + 16 * t;
             uint32_t r = 0;
 #pragma unroll
@@ -1145,65 +1149,208 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         }
         uint32_t etot;
         const uint32_t eoff = wg_excl_sum<256>(e, tmp, &etot);
-        // emit into the LDS copy (o: block-relative output position)
-        uint32_t o = o_carry + eoff;
-        uint32_t un = u0;
+        if (MODE == 1) {
+            // emit into the LDS copy (o: block-relative output position)
+            uint32_t o = o_carry + eoff;
+            uint32_t un = u0;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const uint64_t i = a + q;
-            uint32_t u = un;
-            un = u == 254u ? 0u : u + 1u;
-            if (i < p1) {
-                const uint32_t pv = q ? v[q - 1] : prev;
-                if (i == p0 || v[q] != pv) {
-                    u = 0;
-                    un = 1;
-                }
-                const uint32_t nx = q < 15 ? v[q + 1] : nextb;
-                const bool last = (i + 1 == p1) || nx != v[q] || u == 254;
-                if (u < 3) {
-                    tout[o - o_carry] = v[q];
-                    o++;
-                } else if (u == 3) {
-                    tout[o - o_carry] = v[q];
-                    if (last) tout[o + 1 - o_carry] = 0;  // else the piece's last byte fills the slot
-                    o += 2;
-                } else if (last) {
-                    if (o - 1 >= o_carry) tout[o - 1 - o_carry] = (uint8_t)(u - 3);
-                    else out[o - 1] = (uint8_t)(u - 3);  // piece begun in an earlier tile
+            for (int q = 0; q < 16; ++q) {
+                const uint64_t i = a + q;
+                uint32_t u = un;
+                un = u == 254u ? 0u : u + 1u;
+                if (i < p1) {
+                    const uint32_t pv = q ? v[q - 1] : prev;
+                    if (i == p0 || v[q] != pv) {
+                        u = 0;
+                        un = 1;
+                    }
+                    const uint32_t nx = q < 15 ? v[q + 1] : nextb;
+                    const bool last = (i + 1 == p1) || nx != v[q] || u == 254;
+                    if (u < 3) {
+                        tout[o - o_carry] = v[q];
+                        o++;
+                    } else if (u == 3) {
+                        tout[o - o_carry] = v[q];
+                        if (last) tout[o + 1 - o_carry] = 0;  // else the piece's last byte fills the slot
+                        o += 2;
+                    } else if (last) {
+                        if (o - 1 >= o_carry) tout[o - 1 - o_carry] = (uint8_t)(u - 3);
+                        else out[o - 1] = (uint8_t)(u - 3);  // piece begun in an earlier tile
+                    }
                 }
             }
+            __syncthreads();
+            for (uint32_t j = t; j < etot; j += 256) out[o_carry + j] = tout[j];
         }
-        __syncthreads();
-        for (uint32_t j = t; j < etot; j += 256) out[o_carry + j] = tout[j];
         o_carry += etot;
         if (tot) rs_carry = p0 + tot - 1;
         __syncthreads();
     }
-    if (t == 0) lens[lb] = o_carry;
-    // ordered combination of the accumulators: level l joins neighbours of
-    // 16 * 2^l padded bytes each (in-wave levels by shuffles, then LDS)
-    uint32_t v = acc;
+    if (MODE == 1) {
+        // ordered combination of the accumulators: level l joins neighbours of
+        // 16 * 2^l padded bytes each (in-wave levels by shuffles, then LDS)
+        uint32_t v = acc;
 #pragma unroll
-    for (int l = 0; l < 6; ++l) {
-        const uint32_t right = (uint32_t)__shfl_down((int)v, 1 << l);
-        if ((t & ((2 << l) - 1)) == 0) v = crc_map(crc_tabs + kCrcShiftBase + 1024 * (l + 4), v) ^ right;
+        for (int l = 0; l < 6; ++l) {
+            const uint32_t right = (uint32_t)__shfl_down((int)v, 1 << l);
+            if ((t & ((2 << l) - 1)) == 0) v = crc_map(crc_tabs + kCrcShiftBase + 1024 * (l + 4), v) ^ right;
+        }
+        if ((t & 63) == 0) lastv[t >> 6] = v;
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t* A1024 = crc_tabs + kCrcShiftBase + 1024 * 10;
+            const uint32_t* A2048 = crc_tabs + kCrcShiftBase + 1024 * 11;
+            const uint32_t left = crc_map(A1024, lastv[0]) ^ lastv[1];
+            const uint32_t right = crc_map(A1024, lastv[2]) ^ lastv[3];
+            *raw = crc_map(A2048, left) ^ right;
+        }
     }
-    if ((t & 63) == 0) lastv[t >> 6] = v;
-    __syncthreads();
+    return o_carry - o0;
+}
+
+// the raw register x processed over `len` zero bytes (A_len, binary powers)
+__device__ __forceinline__ uint32_t crc_shift(const uint32_t* __restrict__ crc_tabs, uint32_t x, uint64_t len) {
+    for (int k = 0; k < 32 && (len >> k); ++k)
+        if ((len >> k) & 1u) x = crc_map(crc_tabs + kCrcShiftBase + 1024 * k, x);
+    return x;
+}
+
+// Segments of the batch's blocks (one workgroup): a block of at least
+// 2 kFeSegLen raw bytes is cut near every kFeSegLen bytes at a clean cut (see
+// FeSeg); segs[] in block order, segfirst[lb] its first segment,
+// segfirst[count] = *nseg the total.  rsb[c]: start of the run holding the
+// byte before chunk c (fe_runscan_kernel).
+__global__ __launch_bounds__(1024) void fe_segplan_kernel(const uint8_t* __restrict__ x, uint64_t n,
+                                                          const uint64_t* __restrict__ starts, uint64_t first,
+                                                          uint64_t count, const uint64_t* __restrict__ rsb,
+                                                          const uint4* __restrict__ summ, FeSeg* __restrict__ segs,
+                                                          uint32_t* __restrict__ segfirst, uint64_t seg_cap,
+                                                          uint32_t* __restrict__ nseg) {
+    __shared__ uint32_t tmp[16];
+    const int t = threadIdx.x;
+    // cut j >= 1 of block [p0, p1) is near the chunk boundary q at or after
+    // p0 + j kFeSegLen (only while q + 256 < p1); the cut is q itself when a
+    // run starts there, else the next piece boundary of the run that goes on
+    // through q -- or the run's end, if that comes first (the chunk
+    // summary's first run start): O(1) from the summaries, no byte scans
+    auto cut_at = [&](uint64_t p0, uint64_t j) -> uint64_t {
+        const uint64_t want = p0 + j * kFeSegLen;
+        return (want + kFeChunk - 1) / kFeChunk * kFeChunk;
+    };
+    auto clean = [&](uint64_t p0, uint64_t q) -> uint64_t {
+        const uint64_t c = q / kFeChunk;
+        if (chunk_starts_run(summ, c)) return q;
+        const uint64_t r = max(p0, rsb[c]);
+        const uint32_t ph = (uint32_t)((q - r) % 255u);
+        const uint64_t pb = q + (ph ? 255u - ph : 0u);
+        const uint32_t lead = summ[c].y;  // the chunk's first run start (its length if none)
+        return q + lead < pb ? q + lead : pb;
+    };
+    uint32_t carry = 0;
+    for (uint64_t b0 = 0; b0 < count; b0 += 1024) {
+        const uint64_t lb = b0 + (uint64_t)t;
+        uint32_t k = 0;
+        uint64_t p0 = 0, p1 = 0;
+        if (lb < count) {
+            p0 = starts[first + lb];
+            p1 = starts[first + lb + 1];
+            k = 1;
+            if (p1 - p0 >= 2ull * kFeSegLen)
+                while (cut_at(p0, k) + 256 < p1) ++k;
+        }
+        uint32_t tot;
+        const uint32_t off = carry + wg_excl_sum<1024>(k, tmp, &tot);
+        if (lb < count) {
+            segfirst[lb] = off;
+            uint64_t lo = p0;
+            for (uint32_t j = 1; j <= k; ++j) {
+                const uint64_t hi = j < k ? clean(p0, cut_at(p0, j)) : p1;
+                if (off + j - 1 < seg_cap) segs[off + j - 1] = FeSeg{lo, hi, (uint32_t)lb, j - 1};
+                lo = hi;
+            }
+        }
+        carry += tot;
+        __syncthreads();
+    }
     if (t == 0) {
-        const uint32_t* A1024 = crc_tabs + kCrcShiftBase + 1024 * 10;
-        const uint32_t* A2048 = crc_tabs + kCrcShiftBase + 1024 * 11;
-        const uint32_t left = crc_map(A1024, lastv[0]) ^ lastv[1];
-        const uint32_t right = crc_map(A1024, lastv[2]) ^ lastv[3];
-        const uint32_t raw = crc_map(A2048, left) ^ right;
-        // the initial register 0xffffffff processed over the block's length
-        uint32_t init = 0xffffffffu;
-        const uint64_t len = p1 - p0;
-        for (int k = 0; k < 40 && (len >> k); ++k)
-            if ((len >> k) & 1u) init = crc_map(crc_tabs + kCrcShiftBase + 1024 * k, init);
-        crcs[lb] = ~(init ^ raw);
+        segfirst[count] = carry;
+        *nseg = carry <= seg_cap ? carry : (uint32_t)seg_cap;
     }
+    (void)x;
+    (void)n;
+}
+
+// mode 0: emission counts of the segments that have a successor; mode 1:
+// emission into the block (at the earlier segments' counts), lens, and the CRC
+// (whole blocks) or the segment's raw CRC (cut blocks).  One workgroup per
+// segment; workgroups past *nseg return.
+__global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict__ x, uint64_t n,
+                                                      const FeSeg* __restrict__ segs,
+                                                      const uint32_t* __restrict__ segfirst,
+                                                      const uint32_t* __restrict__ nseg, uint32_t* __restrict__ segcnt,
+                                                      uint32_t* __restrict__ segcrc, int mode,
+                                                      uint8_t* __restrict__ blocks, size_t stride,
+                                                      uint32_t* __restrict__ lens, uint32_t* __restrict__ crcs,
+                                                      const uint32_t* __restrict__ crc_tabs) {
+    __shared__ uint4 tin4[2 * kTile / 16 + 4];
+    __shared__ uint8_t tout[kTileOut];
+    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t lastv[256];
+    __shared__ uint32_t tslice[1024], t4096[1024];
+    __shared__ uint32_t rawv;
+    const uint32_t w = blockIdx.x;
+    if (w >= uniform(*nseg)) return;
+    const FeSeg sg = segs[w];
+    const uint32_t lb = uniform(sg.lb), si = uniform(sg.s);
+    const uint32_t f0 = uniform(segfirst[lb]), k = uniform(segfirst[lb + 1]) - f0;
+    const uint64_t lo = uniform64(sg.lo), hi = uniform64(sg.hi);
+    const int t = threadIdx.x;
+    if (mode == 0) {
+        if (si + 1 >= k) return;  // the last segment's count is not needed
+        const uint32_t e = rle1_range<0>(x, n, lo, hi, nullptr, 0, nullptr, nullptr, nullptr, crc_tabs, tin4, tout,
+                                         tmp, lastv);
+        if (t == 0) segcnt[w] = e;
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        tslice[t + 256 * q] = crc_tabs[t + 256 * q];
+        t4096[t + 256 * q] = crc_tabs[kCrcShiftBase + 1024 * 12 + t + 256 * q];
+    }
+    uint32_t o0 = 0;
+    for (uint32_t j = 0; j < si; ++j) o0 += segcnt[f0 + j];
+    o0 = uniform(o0);
+    __syncthreads();
+    const uint32_t e = rle1_range<1>(x, n, lo, hi, blocks + (size_t)lb * stride, o0, &rawv, tslice, t4096, crc_tabs,
+                                     tin4, tout, tmp, lastv);
+    if (t == 0) {
+        if (si + 1 == k) lens[lb] = o0 + e;
+        if (k == 1) {
+            // the initial register 0xffffffff processed over the block's length
+            crcs[lb] = ~(crc_shift(crc_tabs, 0xffffffffu, hi - lo) ^ rawv);
+        } else {
+            segcrc[w] = rawv;
+        }
+    }
+}
+
+// CRCs of the cut blocks from their segments' raw registers (a thread per block)
+__global__ __launch_bounds__(256) void fe_crccomb_kernel(const FeSeg* __restrict__ segs,
+                                                         const uint32_t* __restrict__ segfirst, uint64_t count,
+                                                         const uint32_t* __restrict__ segcrc,
+                                                         uint32_t* __restrict__ crcs,
+                                                         const uint32_t* __restrict__ crc_tabs) {
+    const uint64_t lb = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lb >= count) return;
+    const uint32_t f0 = segfirst[lb], k = segfirst[lb + 1] - f0;
+    if (k < 2) return;
+    uint32_t raw = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+        const FeSeg sg = segs[f0 + j];
+        raw = crc_shift(crc_tabs, raw, sg.hi - sg.lo) ^ segcrc[f0 + j];
+    }
+    const uint64_t p0 = segs[f0].lo, p1 = segs[f0 + k - 1].hi;
+    crcs[lb] = ~(crc_shift(crc_tabs, 0xffffffffu, p1 - p0) ^ raw);
 }
 
 }  // namespace bz2mi

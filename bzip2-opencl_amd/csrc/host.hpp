@@ -70,8 +70,17 @@ struct FrontBufs {
     uint64_t* d_starts = nullptr;
     uint64_t* d_nb = nullptr;  // [0] blocks, [1] chain status, [2] exit token
     uint64_t* d_agg = nullptr;  // scan tile aggregates
+    // RLE1 emission segments (frontend.hip FeSeg): table, per-block first
+    // entry, total, per-segment emission counts and raw CRCs
+    uint8_t* d_seg = nullptr;
+    uint32_t* d_segfirst = nullptr;
+    uint32_t* d_nseg = nullptr;
+    uint32_t* d_segcnt = nullptr;
+    uint32_t* d_segcrc = nullptr;
+    size_t seg_cap = 0;
     std::vector<void*> ptrs() const {
-        return {d_dmap, d_lane, d_summ, d_rsb, d_ccost, d_fc, d_bnd, d_starts, d_nb, d_agg};
+        return {d_dmap, d_lane, d_summ, d_rsb, d_ccost, d_fc, d_bnd, d_starts, d_nb, d_agg,
+                d_seg, d_segfirst, d_nseg, d_segcnt, d_segcrc};
     }
 };
 

@@ -226,9 +226,21 @@ __global__ void fe_chain_kernel(const uint8_t* x, const uint32_t* laneinfo, cons
 __global__ void fe_resolve_kernel(const uint8_t* x, const uint32_t* laneinfo, const uint64_t* fc, const uint4* summ,
                                   uint64_t n, uint64_t nc, uint64_t n_own, uint64_t entry, const uint64_t* bnd,
                                   uint64_t* nb_io, uint64_t* starts);
-// RLE1 emission + block CRCs (crc_tabs: rle1.hpp crc_device_tables)
-__global__ void fe_rle1_kernel(const uint8_t* x, uint64_t n, const uint64_t* starts, uint64_t first, uint64_t count,
-                               uint8_t* blocks, size_t stride, uint32_t* lens, uint32_t* crcs,
-                               const uint32_t* crc_tabs);
+// RLE1 emission + block CRCs (crc_tabs: rle1.hpp crc_device_tables); blocks
+// of >= 2 kFeSegLen raw bytes are cut into segments of ~kFeSegLen emitted by
+// workgroups of their own (fe_segplan_kernel, two fe_rle1_kernel passes,
+// fe_crccomb_kernel)
+constexpr uint64_t kFeSegLen = 128 << 10;
+struct FeSeg;
+__global__ void fe_segplan_kernel(const uint8_t* x, uint64_t n, const uint64_t* starts, uint64_t first,
+                                  uint64_t count, const uint64_t* rsb, const uint4* summ, FeSeg* segs,
+                                  uint32_t* segfirst, uint64_t seg_cap, uint32_t* nseg);
+__global__ void fe_rle1_kernel(const uint8_t* x, uint64_t n, const FeSeg* segs, const uint32_t* segfirst,
+                               const uint32_t* nseg, uint32_t* segcnt, uint32_t* segcrc, int mode, uint8_t* blocks,
+                               size_t stride, uint32_t* lens, uint32_t* crcs, const uint32_t* crc_tabs);
+__global__ void fe_crccomb_kernel(const FeSeg* segs, const uint32_t* segfirst, uint64_t count, const uint32_t* segcrc,
+                                  uint32_t* crcs, const uint32_t* crc_tabs);
+// device bytes of one segment-table entry (FeSeg)
+constexpr size_t kFeSegBytes = 24;
 
 }  // namespace bz2mi
