@@ -13,7 +13,8 @@ if kind == "random":
     x = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
 else:
     from bz2mi import synth
-    x = torch.from_numpy(synth.text_bytes(n)).cuda()
+    gen = {"text": synth.text_bytes, "mixed": synth.mixed_bytes, "realtext": synth.realtext_bytes}[kind]
+    x = torch.from_numpy(gen(n)).cuda()
 ctx = bz2mi.Context(9, 10)
 out = torch.empty(n + n // 8 + (1 << 20), dtype=torch.uint8, device="cuda")
 for _ in range(2):
