@@ -1055,7 +1055,8 @@ __device__ __forceinline__ uint32_t lds_tie_round(const uint8_t* __restrict__ T,
         const uint32_t q = (uint32_t)(lane * E + e);
         if (q < t) {
             const uint32_t g = gs[e] > carry ? gs[e] : carry;
-            const uint32_t p = (uint32_t)(((uint64_t)key[e] + D) % (uint32_t)n);
+            uint32_t p = (uint32_t)key[e] + D;  // index < n < 2^17, D < 2^16
+            if (p >= (uint32_t)n) p %= (uint32_t)n;
             key[e] = ((uint64_t)g << (IB + 8 * lds_tie_bytes(IB))) | ((load8(T, n, p) >> (64 - 8 * lds_tie_bytes(IB))) << IB) | q;
         }
     }
@@ -2949,6 +2950,8 @@ __device__ __forceinline__ void dg_push(TextLds& L, uint64_t* dl, bool want, uin
 // the group itself -- a later round may know more), 0 (equal rotations: a
 // periodic block).
 constexpr uint32_t kNoIsa = 0xffffffffu;
+// i + x mod n for i, x < n (no integer division)
+__device__ __forceinline__ uint32_t wrap_n(uint32_t v, int n) { return v >= (uint32_t)n ? v - (uint32_t)n : v; }
 constexpr uint32_t kDefMark = 0x80000000u;
 __device__ __forceinline__ int text_cmp_deferred(const uint8_t* Tl, int n, uint32_t i0, uint32_t i1, uint32_t d,
                                                  uint32_t g, const uint32_t* isa, const uint64_t* dl, uint32_t* link,
@@ -3371,7 +3374,7 @@ __device__ __forceinline__ int text_cmp_plain(const uint8_t* Tl, int n, uint32_t
 __device__ __forceinline__ void dg_place_by_images(const uint8_t* Tl, int n, uint32_t* sa, uint32_t* isa,
                                                    uint8_t* out, uint32_t* orig, uint32_t st, uint32_t m,
                                                    uint32_t x) {
-    auto image = [&](uint32_t k) { return isa[((ld_fresh(sa + st + k) & 0x1ffffu) + x) % (uint32_t)n]; };
+    auto image = [&](uint32_t k) { return isa[wrap_n((ld_fresh(sa + st + k) & 0x1ffffu) + x, n)]; };
     for (uint32_t k = 0; k < m; ++k) {
         const uint32_t mk = ld_fresh(sa + st + k) & 0x1ffffu, key = image(k);
         uint32_t r = 0;
@@ -3467,7 +3470,7 @@ __device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t*
                 const bool mine = (uint32_t)lane < m;
                 const uint32_t me = mine ? ld_fresh(sa + st + lane) & 0x1ffffu : 0u;
                 for (uint32_t x = 1; x < dep; ++x) {
-                    const uint32_t a = mine ? isa[(me + x) % (uint32_t)n] : 0u;
+                    const uint32_t a = mine ? isa[wrap_n(me + x, n)] : 0u;
                     if (!__ballot(mine && a >= kDefMark)) {  // every image placed
                         const uint32_t key = mine ? a : 0xffffffffu;
                         uint32_t r = 0;
@@ -3510,7 +3513,7 @@ __device__ TBK_RES_INL void text_resolve_all(const uint8_t* Tl, int n, uint32_t*
                 const uint32_t st = dg_start(e), m = dg_len(e);
                 bool known = true;
                 for (uint32_t k = 0; k < m && known; ++k)
-                    known = isa[((ld_fresh(sa + st + k) & 0x1ffffu) + x) % (uint32_t)n] < kDefMark;
+                    known = isa[wrap_n((ld_fresh(sa + st + k) & 0x1ffffu) + x, n)] < kDefMark;
                 if (known) {
                     dg_place_by_images(Tl, n, sa, isa, out, orig, st, m, x);
                     lk[g] = kDgDone;
