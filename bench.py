@@ -588,7 +588,9 @@ def bench_units(args, world: int, emit: bool = True):
     def step(gather: bool):
         for g in mine:
             units[g].begin(bufs[g], U, halos[g], ends[g])
-        lay = shard.compress_units(units, owners, args.parallel, args.level, group=ctl)
+        # one rank: every unit assembled in place in the stream buffer
+        lay = shard.compress_units(units, owners, args.parallel, args.level, group=ctl,
+                                   out=out0 if world == 1 else None)
         settled = shard.settle(lay, ctl)
         if gather:
             shard.gather_stream_device(lay, settled, out0, args.level, dst=0)
@@ -648,6 +650,14 @@ def bench_units(args, world: int, emit: bool = True):
     for g in mine:
         for k, v in units[g].stats().items():
             vol[k] += v
+    # rank 0's chains of the last step: speculated units, blocks spliced from
+    # a speculation, blocks chained from the entry
+    spec_sum = {"speculated_units": 0, "spliced_blocks": 0, "chained_blocks": 0}
+    for g in mine:
+        ci = units[g].chain_info()
+        spec_sum["speculated_units"] += int(ci["speculated"])
+        spec_sum["spliced_blocks"] += int(ci["spliced"])
+        spec_sum["chained_blocks"] += int(ci["chained"])
     if rank == 0:
         steps = args.steps
         ms_step = dt / steps * 1e3
@@ -674,6 +684,9 @@ def bench_units(args, world: int, emit: bool = True):
                        "input_bytes_per_gpu": n, "output_bytes": int(out_bytes), "ratio": round(out_bytes / tot_in, 5),
                        "blocks": int(sum(lay.nblocks)), "parallelism": f"dp{world} (block shards of one stream)",
                        "gather_in_step": gather_in, "decode_check": verified,
+                       "assembly": "in place in the stream buffer (one rank)" if lay.out is not None
+                       else "per-unit pieces, settled and gathered",
+                       "speculation": spec_sum,
                        "decode_check_what": "whole stream decoded on rank 0's device, every unit's bytes compared",
                        "shared_gpu_rehearsal": share},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

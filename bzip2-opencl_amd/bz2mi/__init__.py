@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BZ2MI_LIBRARY") or os.path.join(_HERE, "libbz2mi.so")
 
 BZ2MI_OK = 0
-ABI_VERSION = 4  # include/bz2mi.h BZ2MI_ABI_VERSION
+ABI_VERSION = 5  # include/bz2mi.h BZ2MI_ABI_VERSION
 BZ2MI_EINVAL = -1
 BZ2MI_EDEVICE = -2
 BZ2MI_ESPACE = -3
@@ -34,7 +34,8 @@ EXPORTS = (
     "bz2mi_compress", "bz2mi_compress_device", "bz2mi_last_timings", "bz2mi_blocks_done",
     "bz2mi_last_stats", "bz2mi_dcreate", "bz2mi_ddestroy", "bz2mi_dset_flags", "bz2mi_decompress", "bz2mi_decompress_device",
     "bz2mi_dlast_timings", "bz2mi_unit_halo", "bz2mi_unit_create", "bz2mi_unit_destroy", "bz2mi_unit_begin",
-    "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode", "bz2mi_unit_assemble", "bz2mi_unit_timings",
+    "bz2mi_unit_chain", "bz2mi_unit_speculate", "bz2mi_unit_chain_info", "bz2mi_unit_sums", "bz2mi_unit_encode",
+    "bz2mi_unit_assemble", "bz2mi_unit_timings",
     "bz2mi_unit_stats", "bz2mi_host_alloc", "bz2mi_host_free", "bz2mi_unit_begin_host", "bz2mi_unit_assemble_host",
     "bz2mi_dstream_reset", "bz2mi_dstream", "bz2mi_dlast_trailing", "bz2mi_abi_version",
 )
@@ -115,13 +116,16 @@ def lib() -> ctypes.CDLL:
     L.bz2mi_unit_destroy.argtypes = [c.c_void_p]
     L.bz2mi_unit_begin.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_size_t, c.c_int, c.c_void_p]
     L.bz2mi_unit_chain.argtypes = [c.c_void_p, c.c_uint64, c.c_uint64, c.POINTER(c.c_uint64), c.POINTER(c.c_uint64)]
+    L.bz2mi_unit_speculate.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
+    L.bz2mi_unit_chain_info.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
     L.bz2mi_unit_sums.argtypes = [c.c_void_p, c.c_void_p]
     L.bz2mi_unit_encode.argtypes = [c.c_void_p, c.c_void_p, c.POINTER(c.c_uint64), c.POINTER(c.c_uint32)]
     L.bz2mi_unit_assemble.argtypes = [c.c_void_p, c.c_uint64, c.c_uint32, c.c_int, c.c_void_p, c.c_size_t,
                                       c.POINTER(c.c_size_t), c.c_void_p]
     L.bz2mi_unit_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float)]
     L.bz2mi_unit_stats.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
-    for name in ("bz2mi_unit_begin", "bz2mi_unit_chain", "bz2mi_unit_sums", "bz2mi_unit_encode",
+    for name in ("bz2mi_unit_begin", "bz2mi_unit_chain", "bz2mi_unit_speculate", "bz2mi_unit_chain_info",
+                 "bz2mi_unit_sums", "bz2mi_unit_encode",
                  "bz2mi_unit_assemble", "bz2mi_unit_timings", "bz2mi_unit_stats"):
         getattr(L, name).restype = c.c_int
     # debugging entry points (not in include/bz2mi.h)
@@ -281,6 +285,18 @@ class Unit:
 
     def begin(self, d_ptr: int, n_own: int, n_halo: int, flags: int = 0, stream: int = 0) -> None:
         _check(lib().bz2mi_unit_begin(self._h, d_ptr, n_own, n_halo, flags, ctypes.c_void_p(stream)))
+
+    def speculate(self) -> int:
+        """bz2mi_unit_speculate: chain from the unit's first byte while the
+        entry is on its way; returns the speculative block count."""
+        nb = ctypes.c_uint64(0)
+        _check(lib().bz2mi_unit_speculate(self._h, ctypes.byref(nb)))
+        return nb.value
+
+    def chain_info(self) -> dict:
+        v = (ctypes.c_uint64 * 4)()
+        _check(lib().bz2mi_unit_chain_info(self._h, v))
+        return {"spec_blocks": v[0], "spliced": v[1], "chained": v[2], "speculated": bool(v[3])}
 
     def chain(self, entry: int, first_block: int):
         ex = ctypes.c_uint64(0)

@@ -16,7 +16,11 @@ compresses its units with the unit protocol of include/bz2mi.h:
   1. chain   -- the entry of unit g is the exit of unit g-1: one 16-byte token
                 (entry, first block index) per unit, passed in stream order;
                 a rank's blocks start compressing as soon as its chain is done
-                while the token travels on;
+                while the token travels on.  While a rank waits for a token it
+                speculates (bz2mi_unit_speculate): it chains the unit from its
+                own first byte, and the chain from the real entry then runs
+                only until it meets a speculative block start (a block's end
+                depends only on the bytes from its start on);
   2. sums    -- the running sum of the per-unit slot sums (p x 258 uint32)
                 passed in stream order like the chain token: the carried
                 seeds of unit g are the sum over the units before it, and a
@@ -33,7 +37,8 @@ Control messages go over a gloo group (host memory, tens of bytes each); the
 only bulk transfer is the final gather.  The result equals the stream one
 device produces for the concatenated input, byte for byte.
 
-A unit object provides: chain(entry, first_block) -> (exit, nblocks);
+A unit object provides: chain(entry, first_block) -> (exit, nblocks),
+optionally speculate() (before chain);
 sums() -> uint32[p*258]; encode(carried) -> (bits, crc);
 assemble(bit_offset, crc_before, flags) -> piece.  Device units are
 bz2mi.Unit (DeviceUnit below); the tests drive the same protocol with the C
@@ -50,6 +55,7 @@ import torch.distributed as dist
 UNIT_ENDS_STREAM = 1
 UNIT_FIRST = 1
 UNIT_LAST = 2
+UNIT_IN_PLACE = 4
 MIDRUN = 1 << 63
 
 EMPTY_STREAM_TAIL = bytes([0x17, 0x72, 0x45, 0x38, 0x50, 0x90, 0, 0, 0, 0])
@@ -80,6 +86,7 @@ class Layout:
     owners: list = field(default_factory=list)
     empty: bool = False
     pieces: dict = field(default_factory=dict)   # local unit g -> piece (assemble output)
+    out: object = None          # one rank, in-place assembly: the stream buffer holding every unit
 
     @property
     def stream_bytes(self) -> int:
@@ -113,10 +120,15 @@ def _all_gather_rows(rows: np.ndarray, counts: list[int], group) -> list[np.ndar
     return [parts[r][: counts[r]].numpy() for r in range(world)]
 
 
-def compress_units(units: dict, owners: list[int], parallel: int, level: int, group=None) -> Layout:
+def compress_units(units: dict, owners: list[int], parallel: int, level: int, group=None,
+                   speculate: str = "wait", out=None) -> Layout:
     """Run the unit protocol for this rank's units (dict global index -> unit,
     every unit already begun) of a stream of len(owners) units.  Returns the
-    layout with this rank's assembled pieces."""
+    layout with this rank's assembled pieces.  speculate: "wait" (units whose
+    token comes from another rank, while it is on its way), "always" (every
+    unit but the first, before its chain: tests) or "never".  out (one rank,
+    units with assemble_into): the stream buffer; every unit is assembled in
+    place at its bit offset (no pieces, no gather copies)."""
     me = _group_rank(group)
     total = len(owners)
     mine = sorted(units)
@@ -124,14 +136,31 @@ def compress_units(units: dict, owners: list[int], parallel: int, level: int, gr
     # 1. the chain, in stream order: token (entry, first block index)
     token = None
     nblocks_local = {}
+    # units whose token comes from another rank: speculated while it travels
+    waits = [g for g in mine if g > 0 and owners[g - 1] != me and hasattr(units[g], "speculate")]
+    if speculate == "never":
+        waits = []
+    speculated = set()
     for g in mine:
+        if speculate == "always" and g > 0 and hasattr(units[g], "speculate"):
+            units[g].speculate()
+            speculated.add(g)
         if g == 0:
             entry, first = 0, 0
         elif owners[g - 1] == me:
             entry, first = token
         else:
             t = torch.zeros(2, dtype=torch.int64)
-            dist.recv(t, src=owners[g - 1], group=group, tag=g)
+            w = dist.irecv(t, src=owners[g - 1], group=group, tag=g)
+            # this unit first, then the later ones, as long as the token is out
+            for h in waits:
+                if h < g or h in speculated:
+                    continue
+                if w.is_completed():
+                    break
+                units[h].speculate()
+                speculated.add(h)
+            w.wait()
             entry, first = int(t[0]) & 0xFFFFFFFFFFFFFFFF, int(t[1])
         ex, nb = units[g].chain(entry, first)
         nblocks_local[g] = nb
@@ -148,6 +177,7 @@ def compress_units(units: dict, owners: list[int], parallel: int, level: int, gr
     acc = None
     rows = np.zeros((len(mine), 3), dtype=np.int64)
     local = _group_size(group) == 1
+    in_place = local and out is not None and all(hasattr(units[g], "assemble_into") for g in mine)
     if local:  # one rank: offsets are known unit by unit too, so it assembles as it goes
         wb_all = [g for g in range(total) if nblocks_local[g] > 0]
         first_u = wb_all[0] if wb_all else -1
@@ -172,7 +202,10 @@ def compress_units(units: dict, owners: list[int], parallel: int, level: int, gr
         if local and nblocks_local[g] > 0:
             offs_l[g], crcb_l[g] = G, C
             flags = (UNIT_FIRST if g == first_u else 0) | (UNIT_LAST if g == last_u else 0)
-            pieces[g] = units[g].assemble(G, C, flags)
+            if in_place:
+                units[g].assemble_into(out, G, C, flags)
+            else:
+                pieces[g] = units[g].assemble(G, C, flags)
             G += bits + (32 if g == first_u else 0)
             C = _rotl(C, nblocks_local[g]) ^ (crc & 0xFFFFFFFF)
     if local:
@@ -182,6 +215,8 @@ def compress_units(units: dict, owners: list[int], parallel: int, level: int, gr
             return Layout(nbl, bl, [-1] * total, [0] * total, -1, -1, 14 * 8, 0, list(owners), empty=True)
         lay = Layout(nbl, bl, offs_l, crcb_l, first_u, last_u, G + 80, C, list(owners))
         lay.pieces = pieces
+        if in_place:
+            lay.out = out
         return lay
     # 3. encode results -> bits, CRC share, blocks
     counts = [sum(1 for o in owners if o == r) for r in range(_group_size(group))]
@@ -264,8 +299,14 @@ class DeviceUnit:
         self.buf = buf  # keep the bytes alive until assembly
         self.unit.begin(buf.data_ptr(), n_own, n_halo, UNIT_ENDS_STREAM if ends else 0, stream)
 
+    def speculate(self):
+        return self.unit.speculate()
+
     def chain(self, entry, first_block):
         return self.unit.chain(entry, first_block)
+
+    def chain_info(self):
+        return self.unit.chain_info()
 
     def sums(self):
         return self.unit.sums()
@@ -285,6 +326,12 @@ class DeviceUnit:
         nbytes = self.unit.assemble(bit_offset, crc_before, flags, self._out.data_ptr(), self._out.numel(), stream)
         return self._out, nbytes
 
+    def assemble_into(self, out: torch.Tensor, bit_offset, crc_before, flags):
+        """In-place assembly into the stream buffer `out` (uint8 device
+        tensor) at stream bit bit_offset; returns the stream bytes so far."""
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        return self.unit.assemble(bit_offset, crc_before, flags | UNIT_IN_PLACE, out.data_ptr(), out.numel(), stream)
+
     def timings(self):
         return self.unit.timings()
 
@@ -302,6 +349,8 @@ def settle(lay: Layout, ctl_group=None) -> dict:
     all-gather over the control group), and the unit keeps the bytes after it.
     Returns {g: (tensor, lo, hi)}: stream bytes [lo, hi) are tensor[0:hi-lo]
     (a view); together the ranks' ranges tile the stream exactly."""
+    if lay.out is not None:  # assembled in place: nothing to settle
+        return {}
     world = _group_size(ctl_group)
     total = len(lay.nblocks)
     wb = [g for g in range(total) if lay.nblocks[g] > 0]
@@ -340,6 +389,11 @@ def gather_stream_device(lay: Layout, settled: dict, out: torch.Tensor | None, l
         e = empty_stream(level)
         out[: len(e)].copy_(torch.frombuffer(bytearray(e), dtype=torch.uint8))
         return out[: len(e)]
+    if lay.out is not None:  # one rank, assembled in place
+        if out is not None and out.data_ptr() != lay.out.data_ptr():
+            out[: lay.stream_bytes].copy_(lay.out[: lay.stream_bytes])
+            return out[: lay.stream_bytes]
+        return lay.out[: lay.stream_bytes]
     total = len(lay.nblocks)
     # the byte ranges of every unit follow from the layout (known everywhere)
     wb = [g for g in range(total) if lay.nblocks[g] > 0]

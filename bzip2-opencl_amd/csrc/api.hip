@@ -107,9 +107,12 @@ int stage_front(bz2mi_ctx* c, Batch& t, const FrontBufs& f, const uint8_t* d_x, 
     hipLaunchKernelGGL(fe_segplan_kernel, dim3(1), dim3(1024), 0, s, d_x, (uint64_t)n, f.d_starts, first, cnt, f.d_rsb,
                        f.d_summ,                       reinterpret_cast<FeSeg*>(f.d_seg), f.d_segfirst, (uint64_t)f.seg_cap, f.d_nseg);
     const unsigned grid = (unsigned)std::min<uint64_t>(f.seg_cap, cnt + n / kFeSegLen + 1);
+    // mode 0 (counts of cut blocks' inner segments): strided over the table
+    const unsigned grid0 = std::min<unsigned>(grid, (unsigned)(4 * c->cus));
     for (int mode = 0; mode < 2; ++mode)
-        hipLaunchKernelGGL(fe_rle1_kernel, dim3(grid), dim3(256), 0, s, d_x, (uint64_t)n, seg, f.d_segfirst, f.d_nseg,
-                           f.d_segcnt, f.d_segcrc, mode, t.d_blocks, c->stride, t.d_lens, t.d_crc, c->d_crctab);
+        hipLaunchKernelGGL(fe_rle1_kernel, dim3(mode ? grid : grid0), dim3(256), 0, s, d_x, (uint64_t)n, seg,
+                           f.d_segfirst, f.d_nseg, f.d_segcnt, f.d_segcrc, mode, t.d_blocks, c->stride, t.d_lens,
+                           t.d_crc, c->d_crctab);
     hipLaunchKernelGGL(fe_crccomb_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, seg, f.d_segfirst, cnt,
                        f.d_segcrc, t.d_crc, c->d_crctab);
     HIPCHECK(hipGetLastError());
@@ -403,6 +406,7 @@ int ensure_front(FrontBufs& f, int S, size_t n) {
     if ((r = dalloc(&f.d_bnd, maxb + 2))) return r;
     if ((r = dalloc(&f.d_starts, maxb + 3))) return r;
     if ((r = dalloc(&f.d_nb, 4))) return r;
+    if ((r = dalloc(&f.d_spec, maxb + 3))) return r;
     // segments: one per block, plus one per kFeSegLen raw bytes of a cut block
     const size_t segs = maxb + cap / bz2mi::kFeSegLen + 8;
     if ((r = dalloc(&f.d_seg, segs * bz2mi::kFeSegBytes))) return r;
@@ -441,31 +445,52 @@ int enqueue_front_scan(FrontBufs& f, const uint8_t* d_x, size_t n, hipStream_t s
     return BZ2MI_OK;
 }
 
+__global__ void copy_u64_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 int run_chain(bz2mi_ctx* c, FrontBufs& f, const uint8_t* d_x, size_t n, size_t n_own, uint64_t entry, bool ends,
-              uint64_t* nb_out, uint64_t* exit_out, hipStream_t s) {
+              uint64_t* nb_out, uint64_t* exit_out, hipStream_t s, uint64_t spec_nb, uint64_t spec_exit,
+              uint64_t* spliced) {
     using namespace bz2mi;
     const uint64_t nc = (n + kFeChunk - 1) / kFeChunk;
+    if (spec_nb > f.maxb) return fail(BZ2MI_EINVAL, "run_chain: speculation longer than the block table");
     hipLaunchKernelGGL(fe_chain_kernel, dim3(1), dim3(kFeChainThreads), 0, s, d_x, f.d_lane, f.d_fc, f.d_summ, f.d_dmap,
                        (uint64_t)n, nc, c->S, (uint64_t)n_own, entry, ends ? 1 : 0, f.d_bnd, (uint64_t)f.maxb,
-                       f.d_nb);
+                       f.d_nb, f.d_spec, spec_nb);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("front-chain");
-    uint64_t hv[2] = {0, 0};
-    HIPCHECK(hipMemcpyAsync(hv, f.d_nb, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    uint64_t hv[4] = {0, 0, 0, 0};
+    HIPCHECK(hipMemcpyAsync(hv, f.d_nb, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
     if (hv[1] == 1) return fail(BZ2MI_EINVAL, "stream unit: the last block runs past the tail halo");
-    if (hv[0] == 0 || hv[0] > f.maxb || hv[1] != 0)
+    const uint64_t J = hv[3];  // merged into the speculative chain at its block J
+    if (hv[1] != 0 || hv[0] > f.maxb || (J == 0 && hv[0] == 0) || (J != 0 && (J >= spec_nb || hv[0] == 0)))
         return fail(BZ2MI_EDEVICE, "front end produced an invalid block count");
-    const uint64_t nb = hv[0];
+    uint64_t nb = hv[0];
     hipLaunchKernelGGL(fe_resolve_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, d_x, f.d_lane, f.d_fc,
                        f.d_summ, (uint64_t)n, nc, (uint64_t)n_own, entry, f.d_bnd, f.d_nb, f.d_starts);
     HIPCHECK(hipGetLastError());
     STAGE_DONE("front-resolve");
-    *nb_out = nb;
-    if (exit_out) {
+    if (spliced) *spliced = 0;
+    if (J) {
+        // starts[nb] == spec[J]: the speculative starts after it and its end
+        const uint64_t tail = spec_nb - J;
+        if (nb + tail > f.maxb) return fail(BZ2MI_EDEVICE, "front end produced an invalid block count");
+        // (a kernel: a DMA copy here measured as waiting for the other streams' work)
+        hipLaunchKernelGGL(copy_u64_kernel, dim3((unsigned)std::min<uint64_t>((tail + 255) / 256, 64)), dim3(256), 0, s,
+                           f.d_spec + J + 1, f.d_starts + nb + 1, tail);
+        HIPCHECK(hipGetLastError());
+        nb += tail;
+        if (spliced) *spliced = tail;
+        if (exit_out) *exit_out = spec_exit;
+        if (hipStreamSynchronize(s) != hipSuccess) return fail(BZ2MI_EDEVICE, "run_chain: splice failed");
+    } else if (exit_out) {
         HIPCHECK(hipMemcpyAsync(exit_out, f.d_nb + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         HIPCHECK(hipStreamSynchronize(s));
     }
+    *nb_out = nb;
     return BZ2MI_OK;
 }
 
@@ -811,14 +836,22 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
     // stages of several batches / stream units are in flight, the kernels that
     // finish a unit are dispatched ahead of the MTF / BWT kernels of later ones
     // (at equal priority the hardware queues served those first and the
-    // units' Huffman kernels formed a tail)
+    // units' Huffman kernels formed a tail).  Stream A (RLE1 emission, BWT:
+    // the long pole) too: the next unit's RLE1 + BWT are dispatched ahead of
+    // the previous unit's MTF (N = 1 unit line 40.4 -> 41.3 GB/s).
     int prio_lo = 0, prio_hi = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->sA, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->sM, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->sB, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->sF, hipStreamNonBlocking) != hipSuccess) {
+    // A/B knob BZ2MI_STREAM_PRIO: five digits for stream, A, M, B, F
+    // (0 default, 1 highest, 2 lowest)
+    int pr[5] = {0, 1, 0, 1, 0};
+    if (const char* e = getenv("BZ2MI_STREAM_PRIO"))
+        for (int i = 0; i < 5 && e[i]; ++i) pr[i] = e[i] - '0';
+    auto mk = [&](hipStream_t* st, int k) {
+        if (pr[k] == 0) return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+        return hipStreamCreateWithPriority(st, hipStreamNonBlocking, pr[k] == 1 ? prio_hi : prio_lo);
+    };
+    if (hipSetDevice(device) != hipSuccess || mk(&c->stream, 0) != hipSuccess || mk(&c->sA, 1) != hipSuccess ||
+        mk(&c->sM, 2) != hipSuccess || mk(&c->sB, 3) != hipSuccess || mk(&c->sF, 4) != hipSuccess) {
         fail(BZ2MI_EDEVICE, "hipStreamCreate failed");
         bz2mi_destroy(c);
         return nullptr;

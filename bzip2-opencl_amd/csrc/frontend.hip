@@ -405,11 +405,9 @@ __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict_
                                                       const uint64_t* __restrict__ rsb, uint64_t n, uint64_t nc,
                                                       const uint64_t* __restrict__ fc, uint8_t* __restrict__ dmap,
                                                       uint32_t* __restrict__ laneinfo) {
-    // staged output position p lives at p + 4 (p / 64): 4 pad bytes every 64,
-    // so the lanes' byte stores (lane l writes near 64 l) fall on distinct
-    // banks instead of two (83 % of the LDS cycles were bank conflicts)
-    __shared__ uint8_t stage[4][kDmapMax + kDmapMax / 16 + 128];  // + one sink byte per lane
-    auto sw = [](uint32_t p) { return p + ((p >> 6) << 2); };
+    // (a padded layout -- 4 bytes every 64, lanes' stores on distinct banks --
+    // removed the bank conflicts but measured 6 % slower: 1.216 vs 1.148 ms)
+    __shared__ uint8_t stage[4][kDmapMax + 64];  // + one sink byte per lane
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wave_id();
     if (c >= nc) return;
     uint8_t* st = stage[wave_id()];
@@ -461,7 +459,7 @@ __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict_
     // the byte flushes nothing); pieces of 2+ bytes (run ends) add the rest.
     const uint64_t span = at <= lim_i ? lim_i - at : 0;
     const uint32_t lim_q = at <= lim_i ? (uint32_t)(span < 63u ? span : 63u) + 1u : 0u;  // bytes q < lim_q have entries
-    const uint32_t sink = (uint32_t)kDmapMax + (uint32_t)kDmapMax / 16 + 64u + (uint32_t)lane;
+    const uint32_t sink = (uint32_t)kDmapMax + (uint32_t)lane;
 #pragma unroll
     for (int q = 0; q < 64; ++q) {
         const uint32_t ci = (kv[q >> 2] >> ((q & 3) * 8)) & 255u;
@@ -470,15 +468,15 @@ __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict_
         const uint32_t kn = (kv[(q + 1) >> 2] >> (((q + 1) & 3) * 8)) & 255u;
         const uint32_t hi = (vn != vq) ? 16u : 0u;
         const bool has = ci != 0 && (uint32_t)q < lim_q;
-        st[has ? sw(fl) : sink] = (uint8_t)(((ci + kn) & 15u) | hi);
+        st[has ? fl : sink] = (uint8_t)(((ci + kn) & 15u) | hi);
         if (has && ci > 1) {
 #pragma unroll
-            for (uint32_t r = 1; r < 5; ++r) st[r < ci ? sw(fl + r) : sink] = (uint8_t)(((ci + kn - r) & 15u) | hi);
+            for (uint32_t r = 1; r < 5; ++r) st[r < ci ? fl + r : sink] = (uint8_t)(((ci + kn - r) & 15u) | hi);
         }
         fl += ci;
     }
     uint8_t* dst = dmap + fc[c];
-    for (uint32_t j = lane; j < ctot; j += 64) dst[j] = st[sw(j)];
+    for (uint32_t j = lane; j < ctot; j += 64) dst[j] = st[j];
 }
 
 namespace {
@@ -635,13 +633,15 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
                                                       const uint8_t* __restrict__ dmap, uint64_t n, uint64_t nc, int S,
                                                       uint64_t n_own, uint64_t entry, int ends,
                                                       uint64_t* __restrict__ bnd, uint64_t max_bnd,
-                                                      uint64_t* __restrict__ nb_out) {
+                                                      uint64_t* __restrict__ nb_out,
+                                                      const uint64_t* __restrict__ spec, uint64_t spec_nb) {
     FeView f{x, laneinfo, fc, summ, n, nc, uniform64(fc[nc])};
     constexpr uint64_t kExpl = 1ull << 63;
     if (n == 0 || n_own == 0) {
         if (threadIdx.x == 0) {
             nb_out[0] = 0;
             nb_out[1] = 0;
+            nb_out[3] = 0;
         }
         return;
     }
@@ -681,6 +681,7 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
     uint64_t exit_b = n | kExpl;
     uint64_t dsum = 0, dcnt = 0;  // (wave 0)
     uint64_t dfp = 8ull << 16;    // mean D, 16.16, for the window predictions
+    uint64_t scur = 1, merged = 0;  // speculation: search cursor, spec index of the merge (0: none)
     [[maybe_unused]] int nwin = 0, nslow = 0;
 #ifdef BZ2MI_PHASES
 #define FE_NOW() wall_clock64()
@@ -972,6 +973,44 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
         __syncthreads();  // trans/walk are rewritten by the next round
         dfp = dfp_next;
         t_bnd += FE_NOW() - t2;
+        // speculation (bz2mi_unit_speculate): spec[0, spec_nb) are the block
+        // starts of the chain from the unit's first byte.  A block's end
+        // depends only on the bytes from its start on, so once a block of this
+        // chain starts where a speculative block starts, the chains agree from
+        // there: stop, the host splices the speculative tail.  One check per
+        // round, on its last block end, with a cursor that only moves forward
+        // (both start lists ascend).
+        if (spec_nb > 1 && !done && k > k0) {
+            if (tid < 64) {
+                const uint64_t b = bnd[k - 1];
+                const uint64_t P = (b >> 63) ? (b & ~kExpl) : ginv(f, b);
+                uint64_t j = scur;
+                bool hit = false;
+                for (;;) {
+                    const uint64_t i = j + (uint64_t)lane_id();
+                    const uint64_t v = i < spec_nb ? spec[i] : ~0ull;
+                    const uint64_t m = __ballot(v >= P);
+                    if (m) {
+                        const int L = __ffsll((long long)m) - 1;
+                        j += (uint64_t)L;
+                        hit = uniform64(__shfl(v, L)) == P;
+                        break;
+                    }
+                    j += 64;
+                }
+                if (tid == 0) {
+                    ctl[0] = j;
+                    ctl[1] = hit ? 1 : 0;
+                }
+            }
+            __syncthreads();
+            scur = ctl[0];
+            if (ctl[1]) {
+                merged = scur;
+                done = true;
+            }
+            __syncthreads();
+        }
     }
 #ifdef BZ2MI_PHASES
     if (threadIdx.x == 0) {
@@ -991,8 +1030,14 @@ __global__ __launch_bounds__(kFeChainThreads) void fe_chain_kernel(const uint8_t
     (void)t_tab, (void)t_ch, (void)t_bnd, (void)t_slow, (void)n_out, (void)n_mid;
 #endif
     if (threadIdx.x == 0) {
-        bnd[k] = exit_b;
-        nb_out[0] = k + 1;
+        if (merged) {  // blocks [0, k) chained, then the speculative blocks from spec[merged]
+            nb_out[0] = k;
+            nb_out[3] = merged;
+        } else {
+            bnd[k] = exit_b;
+            nb_out[0] = k + 1;
+            nb_out[3] = 0;
+        }
         nb_out[1] = status;
     }
 }
@@ -1302,20 +1347,30 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
     __shared__ uint32_t lastv[256];
     __shared__ uint32_t tslice[1024], t4096[1024];
     __shared__ uint32_t rawv;
+    const int t = threadIdx.x;
+    const uint32_t ns = uniform(*nseg);
+    if (mode == 0) {
+        // counts of the segments that have a successor in their block (none
+        // without cut blocks): a small grid striding over the table, so the
+        // pass costs nothing when there is nothing to count (one workgroup per
+        // segment here measured 0.95 ms behind a concurrent MTF kernel)
+        for (uint32_t w = blockIdx.x; w < ns; w += gridDim.x) {
+            const FeSeg sg = segs[w];
+            const uint32_t lb = uniform(sg.lb), si = uniform(sg.s);
+            if (si + 1 >= uniform(segfirst[lb + 1]) - uniform(segfirst[lb])) continue;  // last segment: not needed
+            const uint32_t e = rle1_range<0>(x, n, uniform64(sg.lo), uniform64(sg.hi), nullptr, 0, nullptr, nullptr,
+                                             nullptr, crc_tabs, tin4, tout, tmp, lastv);
+            if (t == 0) segcnt[w] = e;
+            __syncthreads();  // (LDS tiles reused by the next segment)
+        }
+        return;
+    }
     const uint32_t w = blockIdx.x;
-    if (w >= uniform(*nseg)) return;
+    if (w >= ns) return;
     const FeSeg sg = segs[w];
     const uint32_t lb = uniform(sg.lb), si = uniform(sg.s);
     const uint32_t f0 = uniform(segfirst[lb]), k = uniform(segfirst[lb + 1]) - f0;
     const uint64_t lo = uniform64(sg.lo), hi = uniform64(sg.hi);
-    const int t = threadIdx.x;
-    if (mode == 0) {
-        if (si + 1 >= k) return;  // the last segment's count is not needed
-        const uint32_t e = rle1_range<0>(x, n, lo, hi, nullptr, 0, nullptr, nullptr, nullptr, crc_tabs, tin4, tout,
-                                         tmp, lastv);
-        if (t == 0) segcnt[w] = e;
-        return;
-    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         tslice[t + 256 * q] = crc_tabs[t + 256 * q];

@@ -68,7 +68,8 @@ struct FrontBufs {
     uint64_t* d_fc = nullptr;
     uint64_t* d_bnd = nullptr;
     uint64_t* d_starts = nullptr;
-    uint64_t* d_nb = nullptr;  // [0] blocks, [1] chain status, [2] exit token
+    uint64_t* d_nb = nullptr;  // [0] blocks, [1] chain status, [2] exit token, [3] speculation merge index
+    uint64_t* d_spec = nullptr;  // speculative block starts (bz2mi_unit_speculate)
     uint64_t* d_agg = nullptr;  // scan tile aggregates
     // RLE1 emission segments (frontend.hip FeSeg): table, per-block first
     // entry, total, per-segment emission counts and raw CRCs
@@ -79,7 +80,7 @@ struct FrontBufs {
     uint32_t* d_segcrc = nullptr;
     size_t seg_cap = 0;
     std::vector<void*> ptrs() const {
-        return {d_dmap, d_lane, d_summ, d_rsb, d_ccost, d_fc, d_bnd, d_starts, d_nb, d_agg,
+        return {d_dmap, d_lane, d_summ, d_rsb, d_ccost, d_fc, d_bnd, d_starts, d_nb, d_spec, d_agg,
                 d_seg, d_segfirst, d_nseg, d_segcnt, d_segcrc};
     }
 };
@@ -209,8 +210,13 @@ void free_front(FrontBufs& f);
 int enqueue_front_scan(FrontBufs& f, const uint8_t* d_x, size_t n, hipStream_t s);
 // K6-K7: the chain of the unit [0, n_own) of d_x[0, n) from `entry`; *nb_out
 // (host) = blocks, *exit_out = the next unit's entry.  Synchronous on s.
+// With a speculation (spec: f.d_spec[0, spec_nb] = block starts and end of the
+// chain from byte 0, spec_exit its exit token) the chain stops where it meets
+// a speculative block start and the speculative tail is spliced on
+// (*spliced = blocks taken from it).
 int run_chain(bz2mi_ctx* c, FrontBufs& f, const uint8_t* d_x, size_t n, size_t n_own, uint64_t entry, bool ends,
-              uint64_t* nb_out, uint64_t* exit_out, hipStream_t s);
+              uint64_t* nb_out, uint64_t* exit_out, hipStream_t s, uint64_t spec_nb = 0, uint64_t spec_exit = 0,
+              uint64_t* spliced = nullptr);
 int ensure_batch(bz2mi_ctx* c, Batch& t, int nblocks);
 void free_batch(Batch& t);
 int stage_front(bz2mi_ctx* c, Batch& t, const FrontBufs& f, const uint8_t* d_x, size_t n, uint64_t first,

@@ -221,7 +221,8 @@ constexpr int kFeChainThreads = 1024;  // one workgroup
 // first block at `entry` (bit 63: mid-run); out[0] blocks, out[1] status
 __global__ void fe_chain_kernel(const uint8_t* x, const uint32_t* laneinfo, const uint64_t* fc, const uint4* summ,
                                 const uint8_t* dmap, uint64_t n, uint64_t nc, int S, uint64_t n_own, uint64_t entry,
-                                int ends, uint64_t* bnd, uint64_t max_bnd, uint64_t* out);
+                                int ends, uint64_t* bnd, uint64_t max_bnd, uint64_t* out, const uint64_t* spec,
+                                uint64_t spec_nb);
 // starts[0..nb] from the chain; nb_io[2] = exit token of the next unit
 __global__ void fe_resolve_kernel(const uint8_t* x, const uint32_t* laneinfo, const uint64_t* fc, const uint4* summ,
                                   uint64_t n, uint64_t nc, uint64_t n_own, uint64_t entry, const uint64_t* bnd,

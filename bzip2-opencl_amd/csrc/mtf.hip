@@ -454,7 +454,11 @@ void launch_mtf(int nb, const uint8_t* bwt, size_t stride, const uint32_t* lens,
 #ifdef BZ2MI_AB_MTF_WAVES
     const int g = BZ2MI_AB_MTF_WAVES;
 #else
-    const int g = nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : 16;
+    static const int g_env = [] {
+        const char* e = getenv("BZ2MI_MTF_WAVES");  // A/B knob: 1, 2, 4, 8 or 16
+        return e && *e ? atoi(e) : 0;
+    }();
+    const int g = g_env ? g_env : nb >= 6144 ? 1 : nb >= 3072 ? 2 : nb >= 1536 ? 4 : 16;
 #endif
 #define BZ2MI_MTF_LAUNCH(G)                                                                                     \
     hipLaunchKernelGGL(mtf_kernel<G>, dim3(nb), dim3(64 * G), 0, s, bwt, stride, lens, nb, present, mtf_out,      \

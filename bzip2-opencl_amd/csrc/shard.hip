@@ -47,6 +47,11 @@ struct bz2mi_unit {
     uint64_t bits = 0;
     uint32_t crc = 0;
     float chain_ms = 0;
+    // speculation (bz2mi_unit_speculate): the chain from byte 0, its block
+    // count and exit token; chain outcome: blocks taken from it, blocks chained
+    bool spec_tried = false;
+    uint64_t spec_nb = 0, spec_exit = 0;
+    uint64_t spliced = 0, chained = 0;
     hipEvent_t ev_in = nullptr;
     hipEvent_t ev[12] = {};  // stage brackets: front, rle1+bwt, mtf, (seed), huffman, assembly
     uint8_t* d_own = nullptr;  // host-fed units: device copy of the bytes
@@ -65,6 +70,14 @@ bool stage_ok(bz2mi_unit* u, int want) { return u && u->stage >= want; }
 // measured as waiting for work queued on the other streams)
 __global__ void copy_words_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int n) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
+// in-place assembly: the previous unit's bits of the first output word
+// become the carry (MSB-aligned), as advance_kernel carries a batch's last word
+__global__ void carry_in_kernel(bz2mi::StreamDev* __restrict__ st, const uint32_t* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const uint32_t cb = st->carry_bits;
+    st->carry = cb ? __builtin_bswap32(out[st->word_base]) & (0xffffffffu << (32 - cb)) : 0u;
 }
 
 }  // namespace
@@ -134,6 +147,8 @@ int bz2mi_unit_begin(bz2mi_unit* u, const void* d_buf, size_t n_own, size_t n_ha
         return fail(BZ2MI_EINVAL, "stream unit: tail halo shorter than bz2mi_unit_halo()");
     u->nb = 0;
     u->stage = 0;
+    u->spec_tried = false;
+    u->spec_nb = u->spec_exit = u->spliced = u->chained = 0;
     if ((r = ensure_front(u->fe, c->S, u->n))) return r;
     // the bytes were written on the caller's stream (NULL: the null stream)
     HIPCHECK(hipEventRecord(u->ev_in, (hipStream_t)hip_stream));
@@ -143,6 +158,44 @@ int bz2mi_unit_begin(bz2mi_unit* u, const void* d_buf, size_t n_own, size_t n_ha
     if ((r = enqueue_front_scan(u->fe, u->d_x, u->n, c->sF))) return r;
     HIPCHECK(hipEventRecord(u->ev[1], c->sF));
     u->stage = 1;
+    return BZ2MI_OK;
+}
+
+int bz2mi_unit_speculate(bz2mi_unit* u, uint64_t* nblocks) {
+    if (!u || u->stage != 1) return fail(BZ2MI_ESTATE, "bz2mi_unit_speculate: unit not begun or already chained");
+    bz2mi_ctx* c = u->c;
+    if (!u->spec_tried) {
+        HIPCHECK(hipSetDevice(c->device));
+        u->spec_tried = true;
+        HIPCHECK(hipStreamWaitEvent(c->stream, u->ev[1], 0));
+        uint64_t nb = 0, ex = 0;
+        const int r = run_chain(c, u->fe, u->d_x, u->n, u->n_own, 0, u->ends, &nb, &ex, c->stream);
+        if (r == BZ2MI_EINVAL) {
+            // the speculative chain's last block runs past the tail halo: no
+            // speculation (the chain from the real entry decides)
+            (void)hipGetLastError();
+        } else if (r) {
+            return r;
+        } else {
+            // keep its starts [0, nb] (the chain from the entry rewrites d_starts)
+            hipLaunchKernelGGL(copy_words_kernel, dim3((unsigned)std::min<uint64_t>((2 * nb + 257) / 256, 64)), dim3(256),
+                               0, c->stream, reinterpret_cast<const uint32_t*>(u->fe.d_starts),
+                               reinterpret_cast<uint32_t*>(u->fe.d_spec), (int)(2 * (nb + 1)));
+            HIPCHECK(hipGetLastError());
+            u->spec_nb = nb;
+            u->spec_exit = ex;
+        }
+    }
+    if (nblocks) *nblocks = u->spec_nb;
+    return BZ2MI_OK;
+}
+
+int bz2mi_unit_chain_info(bz2mi_unit* u, uint64_t* out4) {
+    if (!u || !out4) return fail(BZ2MI_EINVAL, "null argument");
+    out4[0] = u->spec_nb;
+    out4[1] = u->spliced;
+    out4[2] = u->chained;
+    out4[3] = u->spec_tried ? 1 : 0;
     return BZ2MI_OK;
 }
 
@@ -162,8 +215,23 @@ int bz2mi_unit_chain(bz2mi_unit* u, uint64_t entry, uint64_t first_block, uint64
     int r;
     const auto t0 = std::chrono::steady_clock::now();
     HIPCHECK(hipStreamWaitEvent(c->stream, u->ev[1], 0));
-    uint64_t nb = 0, ex = 0;
-    if ((r = run_chain(c, u->fe, u->d_x, u->n, u->n_own, entry, u->ends, &nb, &ex, c->stream))) return r;
+    uint64_t nb = 0, ex = 0, spl = 0;
+    if (u->spec_nb && p0 == 0) {
+        // the speculation was right: its starts are the chain (a block's split
+        // does not depend on the bytes before its start, so a mid-run flag on
+        // entry 0 changes nothing: the unit's buffer starts a run there)
+        nb = spl = u->spec_nb;
+        ex = u->spec_exit;
+        hipLaunchKernelGGL(copy_words_kernel, dim3((unsigned)std::min<uint64_t>((2 * nb + 257) / 256, 64)), dim3(256), 0,
+                           c->stream, reinterpret_cast<const uint32_t*>(u->fe.d_spec),
+                           reinterpret_cast<uint32_t*>(u->fe.d_starts), (int)(2 * (nb + 1)));
+        HIPCHECK(hipGetLastError());
+    } else if ((r = run_chain(c, u->fe, u->d_x, u->n, u->n_own, entry, u->ends, &nb, &ex, c->stream, u->spec_nb,
+                              u->spec_exit, &spl))) {
+        return r;
+    }
+    u->spliced = spl;
+    u->chained = nb - spl;
     u->chain_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (nb > (uint64_t)INT32_MAX) return fail(BZ2MI_EINVAL, "stream unit: too many blocks");
     u->nb = nb;
@@ -275,6 +343,7 @@ int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before,
     if (((uintptr_t)d_out & 3) != 0) return fail(BZ2MI_EINVAL, "bz2mi_unit_assemble: output not 4-byte aligned");
     bz2mi_ctx* c = u->c;
     const bool first = (flags & BZ2MI_UNIT_FIRST) != 0, last = (flags & BZ2MI_UNIT_LAST) != 0;
+    const bool in_place = (flags & BZ2MI_UNIT_IN_PLACE) != 0;
     if (first && bit_offset != 0) return fail(BZ2MI_EINVAL, "bz2mi_unit_assemble: the first unit starts at bit 0");
     HIPCHECK(hipSetDevice(c->device));
     const int cnt = (int)u->nb;
@@ -284,11 +353,14 @@ int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before,
     if (first) {  // "BZh<level>" (OutputStream.hpp:126-128)
         sd.carry = (0x425a68u << 8) | (uint32_t)('0' + c->level);
         sd.carry_bits = 32;
+    } else if (in_place) {  // from the word holding bit_offset (carry read on the device)
+        sd.word_base = bit_offset >> 5;
+        sd.carry_bits = (uint32_t)(bit_offset & 31);
     } else {
         sd.carry_bits = (uint32_t)(bit_offset & 7);
     }
     sd.crc = crc_before;
-    const uint64_t end = sd.carry_bits + u->bits + (last ? 80u : 0u);
+    const uint64_t end = sd.word_base * 32 + sd.carry_bits + u->bits + (last ? 80u : 0u);
     const uint64_t nbytes = (end + 7) / 8;
     const uint64_t cap_words = cap / 4;
     if (((end + 31) / 32) > cap_words) return fail(BZ2MI_ESPACE, "output buffer too small");
@@ -299,6 +371,8 @@ int bz2mi_unit_assemble(bz2mi_unit* u, uint64_t bit_offset, uint32_t crc_before,
     HIPCHECK(hipStreamWaitEvent(s, u->ev_in, 0));
     HIPCHECK(hipEventRecord(u->ev[9], s));
     HIPCHECK(hipMemcpyAsync(u->d_sd, &sd, sizeof(sd), hipMemcpyHostToDevice, s));
+    if (in_place && !first && sd.carry_bits)
+        hipLaunchKernelGGL(carry_in_kernel, dim3(1), dim3(64), 0, s, u->d_sd, (const uint32_t*)d_out);
     hipLaunchKernelGGL(bz2mi::offsets_dev_kernel, dim3(1), dim3(256), 0, s, t.d_pbits, t.d_crc, cnt, u->d_sd, t.d_offs);
     hipLaunchKernelGGL(bz2mi::assemble_dev_kernel, dim3((unsigned)cnt + 2), dim3(256), 0, s, t.d_payload,
                        c->payload_words, t.d_offs, t.d_crc, cnt, last ? 1 : 0, u->d_sd, (uint32_t*)d_out, cap_words);

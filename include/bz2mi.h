@@ -43,7 +43,7 @@ const char* bz2mi_version(void);
  *   3: bz2mi_unit_assemble / _host gained the trailing hip_stream argument;
  *      bz2mi_decompress* decode the first stream only (the reference)
  *   4: bz2mi_dlast_trailing, bz2mi_abi_version */
-#define BZ2MI_ABI_VERSION 4
+#define BZ2MI_ABI_VERSION 5
 int bz2mi_abi_version(void);
 
 /*
@@ -165,6 +165,12 @@ typedef struct bz2mi_unit bz2mi_unit;
 #define BZ2MI_UNIT_ENDS_STREAM 1 /* begin: the halo reaches the end of the stream */
 #define BZ2MI_UNIT_FIRST 1       /* assemble: stream header first */
 #define BZ2MI_UNIT_LAST 2        /* assemble: end-of-stream trailer last */
+/* assemble in place: d_out is the whole stream's buffer and the unit's bits go
+ * to stream bit bit_offset of it; the bits before it in its first 32-bit word
+ * (the previous unit's, assembled before this call's work runs: same context,
+ * or ordered through hip_stream) are kept.  *out_bytes = the stream's bytes up
+ * to the unit's end.  No copy of the unit's bytes afterwards. */
+#define BZ2MI_UNIT_IN_PLACE 4
 #define BZ2MI_ENTRY_MIDRUN (1ull << 63) /* entry/exit flag: x[p] == x[p-1] in the stream */
 
 /* tail halo bytes a unit needs (the longest raw span of one block) */
@@ -175,6 +181,18 @@ void bz2mi_unit_destroy(bz2mi_unit* u);
  * hip_stream: the stream that wrote them (NULL: the null stream) */
 int bz2mi_unit_begin(bz2mi_unit* u, const void* d_buf, size_t n_own, size_t n_halo, int flags, void* hip_stream);
 int bz2mi_unit_chain(bz2mi_unit* u, uint64_t entry, uint64_t first_block, uint64_t* exit_entry, uint64_t* nblocks);
+/* Speculation (optional, between begin and chain; synchronous): chain the unit
+ * from its own first byte while the real entry is still on its way.  A block's
+ * end depends only on the bytes from its start on (RLE1 restarts at every
+ * block start, OutputStream.hpp:179-188), so bz2mi_unit_chain then chains from
+ * the entry only until one of its blocks starts where a speculative block
+ * starts and takes the remaining blocks from the speculation (all of them when
+ * entry == 0).  The result is the same as without it.  *nblocks (may be NULL) =
+ * the speculative chain's blocks (0: it runs past the tail halo, not used). */
+int bz2mi_unit_speculate(bz2mi_unit* u, uint64_t* nblocks);
+/* after chain: [0] speculative blocks, [1] blocks taken from the speculation,
+ * [2] blocks chained from the entry, [3] 1 if speculated */
+int bz2mi_unit_chain_info(bz2mi_unit* u, uint64_t* out4);
 int bz2mi_unit_sums(bz2mi_unit* u, uint32_t* sums);
 int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, uint32_t* crc);
 /* d_out: device memory, 4-byte aligned, >= (bits + 7 + 32 + 80) / 8 + 4 bytes;

@@ -8,6 +8,7 @@ process and across two gloo ranks; the `gpu` tests run the device units
 from __future__ import annotations
 
 import bz2
+import ctypes
 import os
 import socket
 
@@ -83,6 +84,15 @@ def _free_port() -> int:
     return p
 
 
+class SpecProbeUnit(CpuRefUnit):
+    """A CPU unit with a speculate() that only counts: drives the protocol's
+    token wait (irecv, speculation while the token is out) on gloo ranks."""
+
+    def speculate(self):
+        self.spec_calls = getattr(self, "spec_calls", 0) + 1
+        return 0
+
+
 def _cpu_worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -95,7 +105,7 @@ def _cpu_worker(rank, world, port, q):
     units = {}
     for g, (buf, n_own, n_halo, ends) in enumerate(bufs):
         if owners[g] == rank:
-            u = CpuRefUnit(1, 10, 10000)
+            u = SpecProbeUnit(1, 10, 10000)
             u.begin(buf, n_own, n_halo, ends)
             units[g] = u
     lay = shard.compress_units(units, owners, 10, 1)
@@ -223,6 +233,13 @@ def test_device_units_equal_single_stream(level, p, n):
     whole = o2[:m].cpu().numpy().tobytes()
     assert got == whole
     assert whole == CpuRef().compress(data, level, p)
+    # in-place assembly (BZ2MI_UNIT_IN_PLACE): every unit written at its bit
+    # offset into one stream buffer, the shared boundary words carried over
+    units = _device_units(ctx, x, cuts, owners, 0, level)
+    o3 = torch.full((cap,), 0xA5, dtype=torch.uint8, device=dev)
+    lay3 = shard.compress_units(units, owners, p, level, out=o3)
+    assert lay3.out is not None and not lay3.pieces
+    assert shard.gather_stream_device(lay3, shard.settle(lay3), None, level).cpu().numpy().tobytes() == whole
 
 
 def _gpu_worker(rank, world, port, q):
@@ -264,3 +281,117 @@ def test_device_two_ranks_one_stream():
         p.join(timeout=60)
     assert res == (True, True, True)
     assert all(p.exitcode == 0 for p in procs)
+
+
+# ------------------------------------------------------- speculation ----
+
+def _split_starts(data: bytes, S: int) -> list[int]:
+    """Block starts of the RLE1 split of `data` (the C restatement)."""
+    L = CpuRef().L
+    mx = len(data) // (S - 6) * 2 + 16
+    st = (ctypes.c_uint64 * mx)()
+    nb = L.cpuref_split(data, len(data), S, None, 0, st, None, None, mx)
+    assert nb > 0
+    return list(st[:nb])
+
+
+def _spec_case():
+    """A stream and cuts for speculation (bz2mi_unit_speculate): a chain's
+    offset is kept block after block in RLE1-output units, so two chains meet
+    only where a few bytes of offset vanish in 5-byte run flushes -- here a
+    region of runs of 4.  Units: entry 1 and 3 bytes into the unit just before
+    such flushes (the chains merge), a cut on a block start (the speculation
+    is the chain), cuts inside a long zero run (mid-run entries) and in
+    random / text data (the speculation mispredicts and never merges)."""
+    quad = np.repeat(np.tile(np.array([0x61, 0x62], dtype=np.uint8), 50_000), 4)
+    parts = [synth.random_bytes(300_000, 41), quad, synth.runs_bytes(1_500_000, 42), synth.random_bytes(300_000, 43),
+             np.zeros(800_000, dtype=np.uint8), synth.text_bytes(500_000, 44), synth.runs_bytes(1_000_000, 45)]
+    data = np.concatenate(parts).tobytes()
+    S = 10000
+    allst = _split_starts(data, S)
+    cuts = [[s for s in allst if s > 250_000][0] - 1, [s for s in allst if s > 1_000_000][0] - 3,
+            [s for s in allst if s > 2_000_000][0], 2_900_000, 3_100_000, 3_700_000]
+    halo = bz2mi.unit_halo(1, 10000)
+    bounds = [0] + cuts + [len(data)]
+    expect = []  # per unit: (true blocks, entry, index of the first start shared with the chain from byte 0)
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        tr = [s - a for s in allst if a <= s < b]
+        sp = set(s for s in _split_starts(data[a:min(len(data), b + halo)], S) if s < b - a)
+        entry = min([s for s in allst if s >= a], default=len(data)) - a
+        expect.append((len(tr), entry, next((i for i, s in enumerate(tr) if s in sp), None)))
+    return data, cuts, expect
+
+
+def test_spec_case_layout():
+    """The speculation layout has what the device test needs (C restatement):
+    merging units, an exact one and mispredicting ones."""
+    _, cuts, expect = _spec_case()
+    merging = [g for g, (nb, e, first) in enumerate(expect) if e > 0 and first is not None and first + 2 < nb]
+    exact = [g for g, (nb, e, first) in enumerate(expect) if g > 0 and e == 0]
+    never = [g for g, (nb, e, first) in enumerate(expect) if nb > 0 and first is None]
+    assert merging and exact and len(never) >= 2, expect
+
+
+def _spec_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    data, cuts, _ = _spec_case()
+    x = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    ctx = bz2mi.Context(1, 10, 10000)
+    owners = shard.interleaved_owners(len(cuts) + 1, world)
+    units = _device_units(ctx, x, cuts, owners, rank, 1)
+    lay = shard.compress_units(units, owners, 10, 1, speculate="always")
+    info = {g: units[g].chain_info() for g in units}
+    for g in list(lay.pieces):
+        t, nb = lay.pieces[g]
+        lay.pieces[g] = t[:nb].cpu().numpy().tobytes()
+    got = shard.gather_stream_host(lay, 1)
+    infos = [None] * world
+    dist.all_gather_object(infos, info)
+    if rank == 0:
+        allinfo = {}
+        for d in infos:
+            allinfo.update(d)
+        q.put((got == bz2mi.compress(data, 1, 10), got == CpuRef().compress(data, 1, 10), lay.nblocks, allinfo))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not have_gpu(), reason="needs a HIP device")
+@pytest.mark.timeout(600)
+def test_device_two_ranks_speculation():
+    """Two gloo ranks on cuda:0, every unit speculated: units cut mid-run and
+    mid-block whose speculation mispredicts, merges or is exact -> the single
+    stream, and the chain outcomes agree with the C restatement's chains."""
+    _, _, expect = _spec_case()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spec_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    same_gpu, same_ref, nblocks, info = q.get(timeout=500)
+    for p in procs:
+        p.join(timeout=60)
+    assert same_gpu and same_ref
+    assert all(p.exitcode == 0 for p in procs)
+    merged = 0
+    for g, (nb, entry, first) in enumerate(expect):
+        assert nblocks[g] == nb, (g, nblocks[g], nb)
+        if g == 0 or nb == 0:
+            continue
+        i = info[g]
+        assert i["speculated"], (g, i)
+        assert i["spliced"] + i["chained"] == nb, (g, i)
+        if entry == 0:
+            assert i["spliced"] == nb and i["chained"] == 0, (g, i)  # the speculation is the chain
+        elif first is None:
+            assert i["spliced"] == 0, (g, i)  # mispredicted: the chain from the entry runs in full
+        else:
+            # merged (checked once per chain round): chained at least up to the first shared start
+            assert i["spliced"] == 0 or i["chained"] >= first, (g, i)
+            merged += i["spliced"] > 0
+    assert merged >= 1, info
