@@ -318,6 +318,12 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
                            t.d_sa, t.d_bwt, t.d_orig, c->d_scratch, bwt_slot_bytes(c->S), c->S, t.d_groups,
                            t.d_ngroups, t.d_p2list, p2count, pull);
         HIPCHECK(hipGetLastError());
+        if (getenv("BZ2MI_BWT_STATS")) {  // debug: blocks that reached the doubling
+            uint32_t np = 0;
+            HIPCHECK(hipMemcpyAsync(&np, p2count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "[bz2mi] doubling: %u blocks\n", np);
+        }
     } else {
         // grid-wide doubling: every launch returns at once when nothing is left
         DblGrid G{t.d_blocks, c->stride, t.d_lens, t.d_sa, t.d_bwt, t.d_orig, t.d_groups, t.d_ngroups, t.d_p2list,
@@ -1147,6 +1153,7 @@ int bz2mi_debug_phases(int kernel, unsigned long long* out16) {
         case 5: return bz2mi::tbk_resolve_stats(out16);
         case 6: return bz2mi::dbl_stats(out16);
         case 7: return bz2mi::tbk_extra_stats(out16);
+        case 8: return bz2mi::blk_phase_stats(out16);
         default: return BZ2MI_EINVAL;
     }
 }

@@ -34,6 +34,7 @@ BZ2MI_PHASE_TABLE(g_tbk_stat)
 BZ2MI_PHASE_TABLE(g_tbk_res)  // text_resolve sums (PHASES builds)
 BZ2MI_PHASE_TABLE(g_tbk_x)    // text kernel: tie-round and tied-pair wave time (PHASES builds)
 BZ2MI_PHASE_TABLE(g_dbl_stat)  // bwt_finish sums (PHASES builds)
+BZ2MI_PHASE_TABLE(g_blk_phase)  // bwt_block_kernel: per-phase wall time summed over workgroups (PHASES builds)
 #ifdef TBK_TRACE
 __device__ unsigned int* g_tbk_trace;
 #endif
@@ -52,6 +53,15 @@ int tbk_trace(void* p) {
 int tbk_stats(unsigned long long* out) {
 #ifdef BZ2MI_PHASES
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbk_stat), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
+#else
+    (void)out;
+    return 0;
+#endif
+}
+
+int blk_phase_stats(unsigned long long* out) {
+#ifdef BZ2MI_PHASES
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_phase), sizeof(unsigned long long) * 16) == hipSuccess ? 16 : -1;
 #else
     (void)out;
     return 0;
@@ -133,7 +143,7 @@ struct Scratch {
 };
 
 __device__ Scratch carve(uint8_t* base, int S) {
-    Scratch s;
+    Scratch s{};
     uint8_t* p = base;
     const size_t n = (size_t)S;
     s.ka = (uint64_t*)p; p += 8 * n;
@@ -2175,6 +2185,19 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     }
     uint32_t* sa = sa_all + (size_t)b * stride;
     const uint8_t* Tl = reinterpret_cast<const uint8_t*>(L.text);
+#ifdef BZ2MI_PHASES
+    unsigned long long blk_t = wall_clock64();
+    auto blk_mark = [&](int k) {
+        __syncthreads();
+        if (t == 0) {
+            const unsigned long long now = wall_clock64();
+            atomicAdd(&g_blk_phase[k], now - blk_t);
+            blk_t = now;
+        }
+    };
+#else
+    auto blk_mark = [](int) {};
+#endif
     // ---- text -> LDS (whole 16-byte chunks: the block buffer is padded),
     // first-byte histogram
     if (t < 256) sh.hist[t] = 0;
@@ -2213,6 +2236,7 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
             return;
         }
     }
+    blk_mark(0);
     // ---- pair path: the kPair largest buckets of > kSmall rotations (ties by
     // byte) get a histogram of their second bytes; wave w < npair turns pair
     // slot w's counts into child cursors (counts and starts kept in registers)
@@ -2278,6 +2302,7 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
     } else if (t < 256) {
         L.pslot[t] = 0xffu;
     }
+    blk_mark(1);
     // ---- first-byte scatter, one 8192-rotation tile at a time (8 per thread);
     // rotations of pair buckets go to their (first, second byte) child
     for (int tile0 = 0; tile0 < n; tile0 += FT * 8) {
@@ -2322,6 +2347,7 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
         if (t < 256) sh.base[t] += L.th[t];
     }
     __syncthreads();
+    blk_mark(2);
     if (t < 256) {  // symbols in use (the MTF symbol map): bit t of the 256-bit set
         const uint64_t m = __ballot(c != 0);
         if (lane_id() == 0) {
@@ -2389,13 +2415,11 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
             __syncthreads();
         }
     }
+    blk_mark(3);
     // ---- the small batches, one wave each, keys from the LDS text; the next
     // batch's SA entries are loaded while the current one is sorted
     constexpr int E = kSmall / 64;
     const int w = wave_id(), lane = lane_id();
-    Scratch s{};
-    s.sa = sa;
-    const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, (uint32_t)b, tl + (size_t)b * tcap, tcount + b};
     auto load_batch = [&](uint32_t k, uint32_t (&pre)[E]) {
         const uint32_t st = sh.bat_start[k], len = sh.bat_len[k] & 0x7fffffffu;
 #pragma unroll
@@ -2404,6 +2428,9 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
             pre[e] = g < len ? sa[st + g] : 0u;
         }
     };
+    Scratch s{};
+    s.sa = sa;
+    const GroupSink sink{nullptr, nullptr, 0, nullptr, nullptr, (uint32_t)b, tl + (size_t)b * tcap, tcount + b};
     uint32_t cur[E];
     if ((uint32_t)w < nbat) load_batch((uint32_t)w, cur);
     for (uint32_t k = (uint32_t)w; k < nbat; k += FW) {
@@ -2415,6 +2442,14 @@ __global__ __launch_bounds__(FT) void bwt_block_kernel(const uint8_t* __restrict
 #pragma unroll
         for (int e = 0; e < E; ++e) cur[e] = nxt[e];
     }
+#ifdef BZ2MI_PHASES
+    blk_mark(4);
+    if (t == 0) {
+        atomicAdd(&g_blk_phase[8], 1ull);
+        atomicAdd(&g_blk_phase[9], (unsigned long long)nbat);
+        atomicAdd(&g_blk_phase[10], (unsigned long long)npair);
+    }
+#endif
 }
 
 

@@ -167,6 +167,7 @@ int mtf_phases(unsigned long long* out);
 int fe_phases(unsigned long long* out);
 int tbk_stats(unsigned long long* out);
 int tbk_extra_stats(unsigned long long* out);
+int blk_phase_stats(unsigned long long* out);
 int tbk_resolve_stats(unsigned long long* out);
 int dbl_stats(unsigned long long* out);
 int tbk_trace(void* host_mapped);

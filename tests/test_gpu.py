@@ -52,8 +52,25 @@ def _repeats(n: int) -> np.ndarray:
     return synth.repeats_bytes(n)
 
 
+def _random_repeats(n: int, seed: int = 0x5EED0909) -> np.ndarray:
+    """Random bytes with copies of earlier stretches (64 B .. 6 KB): blocks of
+    random-like first-byte buckets whose rotations tie far past the tie
+    kernels' depth, so the block path's groups reach prefix doubling (the
+    second pass of bwt_block_kernel writes their final SA entries)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    x = rng.integers(0, 256, size=n, dtype=np.uint8)
+    p = 20_000
+    while p < n - 7000:
+        ln = int(rng.choice([64, 300, 1500, 6000]))
+        src = int(rng.integers(max(0, p - 60_000), p - ln))
+        x[p:p + ln] = x[src:src + ln]
+        p += ln + int(rng.integers(2_000, 40_000))
+    return x
+
+
 def _inputs():
     from bz2mi import synth
+    yield "random_repeats", _random_repeats(3 << 20)
     yield "text", synth.text_bytes(6 << 20)
     yield "realtext", synth.realtext_bytes(6 << 20)
     yield "realtext_repeats", _repeats(4 << 20)

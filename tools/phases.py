@@ -36,3 +36,8 @@ v = list(buf)
 print("fe sums (us): table", v[6] / 100.0, "chase", v[7] / 100.0, "bnd", v[8] / 100.0, "slow", v[9] / 100.0, "ends out", v[10], "mid", v[11])
 print("fe raw: rounds", v[12], "k", v[13], "slow", v[14], "us to end", round((v[15] - v[0]) / 100.0, 1))
 print("timings", ctx.timings())
+L.bz2mi_debug_phases(8, buf)
+v = list(buf)
+if v[8]:
+    print("bwt_block_kernel per block (us): text+hist %.1f pair %.1f scatter %.1f children %.1f batches %.1f; blocks %d, batches/block %.1f, pair buckets/block %.2f"
+          % tuple([v[k] / 100.0 / v[8] for k in range(5)] + [v[8], v[9] / v[8], v[10] / v[8]]))
