@@ -1185,6 +1185,7 @@ __device__ uint32_t rle1_range(const uint8_t* __restrict__ x, uint64_t n, uint64
         const uint32_t u0 = a < p1 ? (uint32_t)((a - cur) % 255u) : 0u;
         // emission counts
         uint32_t e = 0;
+        bool ones = true;  // every byte of the thread's emits itself (u < 3)
         uint32_t u = u0;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -1193,11 +1194,42 @@ __device__ uint32_t rle1_range(const uint8_t* __restrict__ x, uint64_t n, uint64
                 const uint32_t pv = q ? v[q - 1] : prev;
                 if (i == p0 || v[q] != pv) u = 0;
                 e += u < 3 ? 1u : (u == 3 ? 2u : 0u);
+                ones = ones && u < 3;
             }
             u = u == 254u ? 0u : u + 1u;
         }
         uint32_t etot;
         const uint32_t eoff = wg_excl_sum<256>(e, tmp, &etot);
+        // A tile without a run of 4 (random-like data: nearly every tile) is
+        // its own encoding: each thread stores its 16 bytes at o_carry + 16 t
+        // straight from registers -- dword stores when the output offset is
+        // 4-aligned (it is while every earlier tile was verbatim) -- with no
+        // LDS output copy and no byte-wise copy-out.
+        if (MODE == 1 && __syncthreads_and(ones)) {
+            const uint32_t o = o_carry + 16u * (uint32_t)t;
+            const uint32_t cnt = a < p1 ? (uint32_t)min<uint64_t>(16, p1 - a) : 0u;
+            if (cnt == 16 && (o & 3u) == 0) {
+                uint32_t w[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    w[k] = v[4 * k] | ((uint32_t)v[4 * k + 1] << 8) | ((uint32_t)v[4 * k + 2] << 16) |
+                           ((uint32_t)v[4 * k + 3] << 24);
+                if ((o & 15u) == 0) {
+                    *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) *reinterpret_cast<uint32_t*>(out + o + 4 * k) = w[k];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    if ((uint32_t)q < cnt) out[o + q] = v[q];
+            }
+            o_carry += etot;
+            if (tot) rs_carry = p0 + tot - 1;
+            __syncthreads();
+            continue;
+        }
         if (MODE == 1) {
             // emit into the LDS copy (o: block-relative output position)
             uint32_t o = o_carry + eoff;
