@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 measurement set (one gpurun call): bench lines (C2 with the 900 KB
-# mode and the N = 1 unit line + CPU baselines; C3 realtext; 27-symbol text),
+# mode and the N = 1 unit line + CPU baselines; C3 realtext; 27-symbol text;
+# decompression of realtext (C5's workload) and random),
 # rocprofv3 kernel stats, FETCH_SIZE / WRITE_SIZE passes and the SQ/GRBM issue
 # pass (separate --pmc runs, kernel trace only), turned into
 # gpurun_out/$TAG/r05_{traffic,issue}_<name>.json on the box (stamped with the
@@ -17,6 +18,10 @@ timeout -k 10 400 python3 $R/bench.py --data realtext --no-cpu --no-units $STEPS
 echo "realtext: $(python3 -c "import json; d=json.load(open('$O/bench_realtext.json')); print(d['value'], d['ms_per_step'], d['roofline']['stage_ms'], '900k', d['mode_900k']['value'], d['mode_900k']['roofline']['stage_ms'])")"
 timeout -k 10 300 python3 $R/bench.py --data text --no-cpu --no-units --no-900k $STEPS > $O/bench_text.json 2> $O/bench_text.err || { echo BENCH_TXT_FAILED; tail $O/bench_text.err; exit 1; }
 echo "text: $(python3 -c "import json; d=json.load(open('$O/bench_text.json')); print(d['value'], d['ms_per_step'], d['roofline']['stage_ms'])")"
+for d in realtext random; do
+timeout -k 10 300 python3 $R/bench.py --mode decompress --data $d --no-cpu $STEPS > $O/bench_dec_$d.json 2> $O/bench_dec_$d.err || { echo BENCH_DEC_FAILED; tail $O/bench_dec_$d.err; exit 1; }
+echo "decompress $d: $(python3 -c "import json; d=json.loads(open('$O/bench_dec_$d.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d.get('stage_ms'))")"
+done
 fi
 IFS=";" read -ra RS <<< "${RUNS:-random:--data random;realtext:--data realtext;text:--data text;random900k:--data random --unit 100000;realtext900k:--data realtext --unit 100000}"
 for spec in "${RS[@]}"; do
