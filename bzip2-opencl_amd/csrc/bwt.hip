@@ -1254,6 +1254,20 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
                                                     const uint32_t (&pre)[kSmall / 64]) {
     static_assert(E <= kSmall / 64, "slots");
     const int lane = lane_id();
+#ifdef BZ2MI_PHASES
+    // per-phase wave time of the batch sorts of every 64th block (g_blk_phase[11..14])
+    const bool bs_on = (blockIdx.x & 63u) == 0 && lane == 0;
+    unsigned long long bs_t = bs_on ? wall_clock64() : 0ull;
+    auto bs_mark = [&](int k) {
+        if (bs_on) {
+            const unsigned long long now = wall_clock64();
+            atomicAdd(&g_blk_phase[k], now - bs_t);
+            bs_t = now;
+        }
+    };
+#else
+    auto bs_mark = [](int) {};
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) L.base[lane * 4 + j] = 0;
     {
@@ -1303,6 +1317,7 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
             }
         }
     }
+    bs_mark(11);
     // rotations in sub-buckets of > kSub (lane l: sub-buckets 4l..4l+3)
     uint32_t inbig = 0;
 #pragma unroll
@@ -1316,6 +1331,7 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
     // sub-buckets: measured on text, 2 -> 8 saves ~1% of the BWT)
     if (8 * nbig > seg.len) {
         wave_sort_lds_any(T, n, s, seg.start, 0, seg.len, d, sink, bwt, orig, L);
+        bs_mark(14);
         return;
     }
     // small sub-buckets: ranks by counting (striped positions p = e*64 + lane)
@@ -1413,6 +1429,7 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
             sink.push_agg(mine && le - lt >= 2 && eqlt == 0, Seg{seg.start + b0 + lt, le - lt}, d + 8);
         }
     }
+    bs_mark(12);
     if (nbig) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1427,6 +1444,7 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
             }
         }
     }
+    bs_mark(13);
 }
 
 template <class BL>

@@ -41,3 +41,7 @@ v = list(buf)
 if v[8]:
     print("bwt_block_kernel per block (us): text+hist %.1f pair %.1f scatter %.1f children %.1f batches %.1f; blocks %d, batches/block %.1f, pair buckets/block %.2f"
           % tuple([v[k] / 100.0 / v[8] for k in range(5)] + [v[8], v[9] / v[8], v[10] / v[8]]))
+if v[8]:
+    nb64 = max(1, v[8] // 64)
+    print("batch sorts of every 64th block, wave-us per block: sub-buckets %.1f counting %.1f big %.1f whole-segment %.1f"
+          % tuple(v[k] / 100.0 / nb64 for k in (11, 12, 13, 14)))
