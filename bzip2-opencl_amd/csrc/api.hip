@@ -106,7 +106,10 @@ int stage_front(bz2mi_ctx* c, Batch& t, const FrontBufs& f, const uint8_t* d_x, 
     auto* seg = reinterpret_cast<const FeSeg*>(f.d_seg);
     hipLaunchKernelGGL(fe_segplan_kernel, dim3(1), dim3(1024), 0, s, d_x, (uint64_t)n, f.d_starts, first, cnt, f.d_rsb,
                        f.d_summ,                       reinterpret_cast<FeSeg*>(f.d_seg), f.d_segfirst, (uint64_t)f.seg_cap, f.d_nseg);
-    const unsigned grid = (unsigned)std::min<uint64_t>(f.seg_cap, cnt + n / kFeSegLen + 1);
+    // (the emission strides over the segments: one workgroup per block plus
+    // at most 4 per CU for the extra segments of cut blocks)
+    const unsigned grid = (unsigned)std::min<uint64_t>(
+        f.seg_cap, cnt + std::min<uint64_t>(n / kFeSegLen + 1, 4 * (uint64_t)c->cus));
     // mode 0 (counts of cut blocks' inner segments): strided over the table
     const unsigned grid0 = std::min<unsigned>(grid, (unsigned)(4 * c->cus));
     for (int mode = 0; mode < 2; ++mode)
@@ -235,7 +238,7 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
             if (mode == 1 && text_path) {
                 hipLaunchKernelGGL(bwt_text_kernel, dim3(nb), dim3(1024), 0, s, t.d_blocks, c->stride, t.d_lens, nb,
                                    t.d_sa, t.d_bwt, t.d_orig, t.d_redo, c->d_lspill, t.d_groups, c->d_tq[0],
-                                   c->d_tq[1], tcap);
+                                   c->d_tq[1], tcap, c->wq_cap);
                 HIPCHECK(hipGetLastError());
             }
             if (mode == 1 && !text_path) {  // every text-like block back to the general path
@@ -418,6 +421,7 @@ int ensure_front(FrontBufs& f, int S, size_t n) {
     if ((r = dalloc(&f.d_seg, segs * bz2mi::kFeSegBytes))) return r;
     if ((r = dalloc(&f.d_segfirst, maxb + 8))) return r;
     if ((r = dalloc(&f.d_nseg, 4))) return r;
+    HIPCHECK(hipMemset(f.d_nseg, 0, 4 * sizeof(uint32_t)));  // [1]: segment table overflow (sticky)
     if ((r = dalloc(&f.d_segcnt, segs))) return r;
     if ((r = dalloc(&f.d_segcrc, segs))) return r;
     f.seg_cap = segs;
@@ -646,6 +650,7 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
     // pipeline starts; when an allocation fails (another context or process
     // holds much of HBM) every batch buffer is freed and the batch halved
     uint64_t bsz = (uint64_t)c->batch_blocks;
+    bool recovered = false;
     {
         // at most ~80 % of what is free now, counting the buffers this context
         // already holds (they are reused or freed below)
@@ -679,9 +684,12 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
         for (Batch& t : c->sets) free_batch(t);
         free_bwt_scratch(c);
         (void)hipGetLastError();
+        // (halved for this call only: a later call sizes its batch again
+        // from the HBM then free)
         bsz = (want + 1) / 2;
-        c->batch_blocks = (int)bsz;
+        recovered = true;
     }
+    if (recovered) clear_error();
     const uint64_t nbat = nb ? (nb + bsz - 1) / bsz : 1;
     // output: word-aligned destination, else an aligned staging buffer
     uint32_t* out32 = (uint32_t*)d_out;
@@ -747,6 +755,11 @@ int compress_device_impl(bz2mi_ctx* c, const uint8_t* d_x, size_t n, uint8_t* d_
     }
     HIPCHECK(hipMemcpyAsync(&c->h_sd, c->d_sd, sizeof(StreamDev), hipMemcpyDeviceToHost, c->sB));
     HIPCHECK(hipStreamSynchronize(c->sB));
+    {
+        uint32_t segov = 0;
+        HIPCHECK(hipMemcpy(&segov, c->fe.d_nseg + 1, sizeof(segov), hipMemcpyDeviceToHost));
+        if (segov) return fail(BZ2MI_EDEVICE, "front end: RLE1 segment table overflow");
+    }
     const uint64_t bytes = (c->h_sd.final_bits + 7) / 8;
     if (bytes > cap_words * 4) return fail(BZ2MI_ESPACE, "output buffer too small");
     if (staged) HIPCHECK(hipMemcpy(d_out, c->d_ostage, bytes, hipMemcpyDeviceToDevice));
@@ -919,6 +932,9 @@ bz2mi_ctx* bz2mi_create(int level, int parallel_blocks, int unit, int device) {
         c->batch_blocks = std::min(c->batch_blocks, std::max(16, (int)(budget / per)));
     }
     if (const char* e = getenv("BZ2MI_BATCH_BLOCKS")) c->batch_blocks = std::max(1, atoi(e));
+    // test hook: the text kernel's work queue limited to this many ring slots,
+    // so that a push overruns and the block is handed back to the general path
+    if (const char* e = getenv("BZ2MI_DEBUG_WQ_RING")) c->wq_cap = (uint32_t)std::max(1, atoi(e));
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     if (hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess) {
         fail(BZ2MI_EDEVICE, "hipEventCreate failed");

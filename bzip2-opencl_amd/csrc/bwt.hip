@@ -2894,6 +2894,7 @@ struct TextLds {
     uint32_t wlo[FW], whi[FW];        // a wave's range of pair entries (the deal)
     uint32_t qn[2], fail, nflag, ndef, nitems, next_item;  // next_item: the work queue's next dl2 item
     uint32_t wq_head, wq_tail, wq_used, wq_out;  // work queue (BZ2MI_TEXT_WQ): claimed, reserved, read, unfinished
+    uint32_t wq_cap;                  // usable ring slots (kWqRing; fewer under BZ2MI_DEBUG_WQ_RING)
     uint8_t order[256];               // bytes by ascending bucket size
     uint8_t rank[256];                // position of a byte in that order
     uint8_t target[256];
@@ -2955,18 +2956,31 @@ __device__ __forceinline__ void tq_push(TextLds& L, int nxt, bool want, uint32_t
     if (m == 0) return;
     if (nxt == kWqPush) {
         // unfinished count first (a waiting wave must not see 0 while these
-        // items exist), then the slots; a ring that would overrun the slots
-        // not yet read sends the block back
+        // items exist), then the slots.  Slots are reserved only when they
+        // fit (a CAS on the tail against the slots not yet read), so every
+        // reserved position is written right below and a consumer that
+        // claimed one always sees its item; a ring that would overrun
+        // reserves nothing and sends the block back (L.fail: every wave then
+        // leaves the queue loop, whatever wq_out says).
         uint32_t base = 0, over = 0;
         if (lane_id() == 0) {
             const uint32_t c = (uint32_t)__popcll(m);
             atomicAdd(&L.wq_out, c);
-            base = atomicAdd(&L.wq_tail, c);
-            over = base + c - *(volatile uint32_t*)&L.wq_used > kWqRing ? 1u : 0u;
-            if (over) TBK_FAIL(4);
+            uint32_t tl = *(volatile uint32_t*)&L.wq_tail;
+            for (;;) {
+                if (tl + c - *(volatile uint32_t*)&L.wq_used > L.wq_cap) {
+                    over = 1u;
+                    TBK_FAIL(4);
+                    break;
+                }
+                const uint32_t old = atomicCAS(&L.wq_tail, tl, tl + c);
+                if (old == tl) break;
+                tl = old;
+            }
+            base = tl;
         }
         base = uniform(base);
-        if (uniform(over)) return;  // (the block goes back; the slots are not written)
+        if (uniform(over)) return;  // (the block goes back; nothing was reserved)
         if (want) {
             const uint32_t pos = base + (uint32_t)__popcll(m & __lanemask_lt());
             (&L.q[0][0])[pos % kWqRing] = tq_item(start, len, depth) | kWqValid;
@@ -3835,7 +3849,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                                                       uint32_t* __restrict__ orig_out, uint32_t* __restrict__ redo,
                                                       uint32_t* __restrict__ spill_all, Seg* __restrict__ grp_all,
                                                       uint64_t* __restrict__ key_all, uint64_t* __restrict__ glist_all,
-                                                      size_t tcap) {
+                                                      size_t tcap, uint32_t wq_cap) {
     __shared__ TextLds L;
     const int b = blockIdx.x;
     if (b >= nblocks || redo[b] != 1u) return;
@@ -4050,6 +4064,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         L.next_item = 0;
         L.wq_head = L.wq_tail = L.wq_used = 0;
         L.wq_out = nitems;
+        L.wq_cap = wq_cap < kWqRing ? wq_cap : kWqRing;
     }
     for (int k = t; k < (int)kWqRing; k += FT) (&L.q[0][0])[k] = 0;
     __syncthreads();
@@ -4060,15 +4075,18 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
             const uint32_t h = *(volatile uint32_t*)&L.wq_head, tl = *(volatile uint32_t*)&L.wq_tail;
             if (h < tl && atomicCAS(&L.wq_head, h, h + 1) == h) {
                 // claimed ring position h: its item is written right after the
-                // push reserved it
+                // push reserved it (tq_push reserves only slots that fit, so
+                // it comes; the wait also ends when the block has failed)
                 volatile uint64_t* slot = &(&L.q[0][0])[h % kWqRing];
                 uint64_t v;
-                while (!((v = *slot) & kWqValid)) __builtin_amdgcn_s_sleep(1);
-                *slot = 0;
-                atomicAdd(&L.wq_used, 1u);
-                lo32 = (uint32_t)v;
-                hi32 = (uint32_t)(v >> 32) & 0x7fffffffu;
-                got = 1;
+                while (!((v = *slot) & kWqValid) && *(volatile uint32_t*)&L.fail == 0u) __builtin_amdgcn_s_sleep(1);
+                if (v & kWqValid) {
+                    *slot = 0;
+                    atomicAdd(&L.wq_used, 1u);
+                    lo32 = (uint32_t)v;
+                    hi32 = (uint32_t)(v >> 32) & 0x7fffffffu;
+                    got = 1;
+                }
             } else if (h >= tl) {
                 const uint32_t k = atomicAdd(&L.next_item, 1u);
                 if (k < nitems) {

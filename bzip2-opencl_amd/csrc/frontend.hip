@@ -1356,6 +1356,9 @@ __global__ __launch_bounds__(1024) void fe_segplan_kernel(const uint8_t* __restr
     if (t == 0) {
         segfirst[count] = carry;
         *nseg = carry <= seg_cap ? carry : (uint32_t)seg_cap;
+        // a table overflow (the capacity bounds every batch by arithmetic)
+        // leaves blocks unemitted: a sticky flag the host checks
+        if (carry > seg_cap) nseg[1] = 1u;
     }
     (void)x;
     (void)n;
@@ -1397,31 +1400,36 @@ __global__ __launch_bounds__(256) void fe_rle1_kernel(const uint8_t* __restrict_
         }
         return;
     }
-    const uint32_t w = blockIdx.x;
-    if (w >= ns) return;
-    const FeSeg sg = segs[w];
-    const uint32_t lb = uniform(sg.lb), si = uniform(sg.s);
-    const uint32_t f0 = uniform(segfirst[lb]), k = uniform(segfirst[lb + 1]) - f0;
-    const uint64_t lo = uniform64(sg.lo), hi = uniform64(sg.hi);
+    if (blockIdx.x >= ns) return;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         tslice[t + 256 * q] = crc_tabs[t + 256 * q];
         t4096[t + 256 * q] = crc_tabs[kCrcShiftBase + 1024 * 12 + t + 256 * q];
     }
-    uint32_t o0 = 0;
-    for (uint32_t j = 0; j < si; ++j) o0 += segcnt[f0 + j];
-    o0 = uniform(o0);
-    __syncthreads();
-    const uint32_t e = rle1_range<1>(x, n, lo, hi, blocks + (size_t)lb * stride, o0, &rawv, tslice, t4096, crc_tabs,
-                                     tin4, tout, tmp, lastv);
-    if (t == 0) {
-        if (si + 1 == k) lens[lb] = o0 + e;
-        if (k == 1) {
-            // the initial register 0xffffffff processed over the block's length
-            crcs[lb] = ~(crc_shift(crc_tabs, 0xffffffffu, hi - lo) ^ rawv);
-        } else {
-            segcrc[w] = rawv;
+    // segment w, w + grid, ...: the grid is one workgroup per block plus a
+    // bounded number for the cut blocks' extra segments, so nearly every
+    // workgroup takes one segment and none is launched only to return
+    for (uint32_t w = blockIdx.x; w < ns; w += gridDim.x) {
+        const FeSeg sg = segs[w];
+        const uint32_t lb = uniform(sg.lb), si = uniform(sg.s);
+        const uint32_t f0 = uniform(segfirst[lb]), k = uniform(segfirst[lb + 1]) - f0;
+        const uint64_t lo = uniform64(sg.lo), hi = uniform64(sg.hi);
+        uint32_t o0 = 0;
+        for (uint32_t j = 0; j < si; ++j) o0 += segcnt[f0 + j];
+        o0 = uniform(o0);
+        __syncthreads();  // (the CRC tables; the previous segment's LDS tiles)
+        const uint32_t e = rle1_range<1>(x, n, lo, hi, blocks + (size_t)lb * stride, o0, &rawv, tslice, t4096,
+                                         crc_tabs, tin4, tout, tmp, lastv);
+        if (t == 0) {
+            if (si + 1 == k) lens[lb] = o0 + e;
+            if (k == 1) {
+                // the initial register 0xffffffff processed over the block's length
+                crcs[lb] = ~(crc_shift(crc_tabs, 0xffffffffu, hi - lo) ^ rawv);
+            } else {
+                segcrc[w] = rawv;
+            }
         }
+        __syncthreads();
     }
 }
 

@@ -20,6 +20,9 @@ namespace bz2mi {
 namespace host {
 
 inline int fail(int code, const std::string& msg) { return bz2mi_set_error(code, msg); }
+// forget the message of a failure the caller recovered from (a batch halved
+// after an allocation failure, a speculation that ran past its halo)
+inline void clear_error() { (void)bz2mi_set_error(BZ2MI_OK, std::string()); }
 
 #define HIPCHECK(expr)                                                                                  \
     do {                                                                                                \
@@ -145,6 +148,7 @@ struct bz2mi_ctx {
     int cus = 256;
     int bwt_slots = 0;
     int batch_blocks = 0;  // blocks per pipelined batch (0: from the block size)
+    uint32_t wq_cap = 0xffffffffu;  // text kernel work-queue slots (BZ2MI_DEBUG_WQ_RING: fewer, tests)
     bool want_stats = false;
 
     bz2mi::host::Batch sets[bz2mi::host::kSets];

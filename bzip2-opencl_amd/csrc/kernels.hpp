@@ -60,7 +60,7 @@ __global__ void bwt_block_kernel(const uint8_t* blocks, size_t stride, const uin
 __global__ void bwt_text_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                                 uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint32_t* redo,
                                 uint32_t* spill_all, BwtSeg* grp_all, uint64_t* key_all, uint64_t* glist_all,
-                                size_t tcap);
+                                size_t tcap, uint32_t wq_cap);
 __global__ void redo_all_kernel(uint32_t* redo, int nblocks);
 __global__ void bwt_level_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                  uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch, uint32_t* spill_all,

@@ -172,8 +172,10 @@ int bz2mi_unit_speculate(bz2mi_unit* u, uint64_t* nblocks) {
         const int r = run_chain(c, u->fe, u->d_x, u->n, u->n_own, 0, u->ends, &nb, &ex, c->stream);
         if (r == BZ2MI_EINVAL) {
             // the speculative chain's last block runs past the tail halo: no
-            // speculation (the chain from the real entry decides)
+            // speculation (the chain from the real entry decides); an expected
+            // outcome, so its message is not left behind
             (void)hipGetLastError();
+            clear_error();
         } else if (r) {
             return r;
         } else {
@@ -226,6 +228,9 @@ int bz2mi_unit_chain(bz2mi_unit* u, uint64_t entry, uint64_t first_block, uint64
                            c->stream, reinterpret_cast<const uint32_t*>(u->fe.d_spec),
                            reinterpret_cast<uint32_t*>(u->fe.d_starts), (int)(2 * (nb + 1)));
         HIPCHECK(hipGetLastError());
+        // stage_front reads d_starts on stream A: the copy is done first (as
+        // run_chain's own path is synchronous on the context stream)
+        HIPCHECK(hipStreamSynchronize(c->stream));
     } else if ((r = run_chain(c, u->fe, u->d_x, u->n, u->n_own, entry, u->ends, &nb, &ex, c->stream, u->spec_nb,
                               u->spec_exit, &spl))) {
         return r;
@@ -320,15 +325,23 @@ int bz2mi_unit_encode(bz2mi_unit* u, const uint32_t* carried, uint64_t* bits, ui
     bz2mi::StreamDev sd{};
     uint64_t total = 0;
     uint8_t* res = u->h_pin + ne * sizeof(uint32_t);  // (its bytes after the seeds: 256 >= 8 + sizeof(sd))
-    static_assert(sizeof(bz2mi::StreamDev) + 8 <= 256, "pinned result area");
+    static_assert(sizeof(bz2mi::StreamDev) + 12 <= 256, "pinned result area");
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const uint32_t*>(t.d_offs + cnt),
                        reinterpret_cast<uint32_t*>(res), 2);
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const uint32_t*>(u->d_sd),
                        reinterpret_cast<uint32_t*>(res + 8), (int)(sizeof(sd) / 4));
+    // the front end's segment-table overflow flag (fe_segplan_kernel)
+    hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, s, u->fe.d_nseg + 1,
+                       reinterpret_cast<uint32_t*>(res + 8 + sizeof(sd)), 1);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(s));
     std::memcpy(&total, res, sizeof(uint64_t));
     std::memcpy(&sd, res + 8, sizeof(sd));
+    {
+        uint32_t segov = 0;
+        std::memcpy(&segov, res + 8 + sizeof(sd), sizeof(segov));
+        if (segov) return fail(BZ2MI_EDEVICE, "front end: RLE1 segment table overflow");
+    }
     u->bits = total;
     u->crc = sd.crc;
     *bits = total;
