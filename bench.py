@@ -585,12 +585,25 @@ def bench_units(args, world: int, emit: bool = True):
         bound = bz2mi.compress_bound(n * world, args.level, args.unit)
         out0 = torch.empty(bound, dtype=torch.uint8, device=dev)
 
+    # BZ2MI_UNIT_TRACE=<prefix>: every rank writes the host timeline of its
+    # last step (chain token arrivals, chain ends, seed rounds, encodes) to
+    # <prefix>.<rank>.json (tools/unit_hops.py: per-hop latency, critical path)
+    trace_path = os.environ.get("BZ2MI_UNIT_TRACE")
+    trace = [] if trace_path else None
+
     def step(gather: bool):
+        if trace is not None:
+            trace.clear()
+            trace.append(("step", -1, time.perf_counter()))
         for g in mine:
             units[g].begin(bufs[g], U, halos[g], ends[g])
         # one rank: every unit assembled in place in the stream buffer
         lay = shard.compress_units(units, owners, args.parallel, args.level, group=ctl,
-                                   out=out0 if world == 1 else None)
+                                   out=out0 if world == 1 else None, trace=trace,
+                                   seeds=os.environ.get("BZ2MI_SEEDS", "rounds"))
+        if trace is not None:
+            torch.cuda.synchronize()
+            trace.append(("end", -1, time.perf_counter()))
         settled = shard.settle(lay, ctl)
         if gather:
             shard.gather_stream_device(lay, settled, out0, args.level, dst=0)
@@ -611,6 +624,10 @@ def bench_units(args, world: int, emit: bool = True):
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    if trace is not None:
+        with open(f"{trace_path}.{rank}.json", "w") as f:
+            json.dump({"rank": rank, "world": world, "units": total, "unit_bytes": U, "owners": owners,
+                       "events": trace}, f)
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if share else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

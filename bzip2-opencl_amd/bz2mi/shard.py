@@ -46,6 +46,7 @@ restatement's units.
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -120,15 +121,64 @@ def _all_gather_rows(rows: np.ndarray, counts: list[int], group) -> list[np.ndar
     return [parts[r][: counts[r]].numpy() for r in range(world)]
 
 
+def _seed_rounds(units: dict, owners: list[int], mine: list[int], w: int, group, encode,
+                 trace: list | None = None) -> None:
+    """Carried seeds by all-gathers (exchange 1): round j
+    all-gathers the slot sums of every rank's j-th unit (global index + p x 258
+    uint32), and an exclusive scan in stream order over the sums known so far
+    gives the carried seeds of every unit whose predecessors are all known;
+    this rank's such units are encoded right after the round.  With
+    interleaved owners round j completes units [j N, (j+1) N), so a stream of
+    N x k units takes k collectives instead of N k serial token hops, and
+    every unit is still encoded as soon as its round is in."""
+    world = _group_size(group)
+    total = len(owners)
+    rounds = max(sum(1 for o in owners if o == r) for r in range(world))
+    known = {}
+    carried_of = {}
+    acc = np.zeros(w, dtype=np.uint32)
+    k = 0                      # acc = uint32 sum of the sums of units < k
+    todo = list(mine)
+    for j in range(rounds):
+        row = torch.zeros(w + 1, dtype=torch.int64)
+        row[0] = -1
+        if j < len(mine):
+            g = mine[j]
+            row[0] = g
+            row[1:] = torch.from_numpy(units[g].sums().astype(np.uint32).astype(np.int64))
+        parts = [torch.zeros_like(row) for _ in range(world)]
+        dist.all_gather(parts, row, group=group)
+        if trace is not None:
+            trace.append(("round", j, time.perf_counter()))
+        for t in parts:
+            if int(t[0]) >= 0:
+                known[int(t[0])] = t[1:].numpy().astype(np.uint32)
+        while k < total and k in known:
+            carried_of[k] = acc.copy()
+            acc = acc + known.pop(k)   # uint32 wrap-around, as the reference's int array
+            k += 1
+        while todo and todo[0] in carried_of:
+            g = todo.pop(0)
+            encode(g, carried_of.pop(g))
+    assert not todo, "seed rounds left units unencoded"
+
+
 def compress_units(units: dict, owners: list[int], parallel: int, level: int, group=None,
-                   speculate: str = "wait", out=None) -> Layout:
+                   speculate: str = "wait", out=None, seeds: str = "rounds", trace: list | None = None) -> Layout:
     """Run the unit protocol for this rank's units (dict global index -> unit,
     every unit already begun) of a stream of len(owners) units.  Returns the
     layout with this rank's assembled pieces.  speculate: "wait" (units whose
     token comes from another rank, while it is on its way), "always" (every
     unit but the first, before its chain: tests) or "never".  out (one rank,
     units with assemble_into): the stream buffer; every unit is assembled in
-    place at its bit offset (no pieces, no gather copies)."""
+    place at its bit offset (no pieces, no gather copies).  seeds (world > 1):
+    "rounds" (all-gather per round of units, _seed_rounds) or "token" (the
+    running sum passed unit to unit in stream order).  trace: a list that
+    gets (event, unit, time.perf_counter()) for the chain token's arrival
+    ("recv"), every chain's end ("chain"), the seed rounds ("round") and every
+    encode's end ("encode") -- the host timeline of the critical path."""
+    clock = time.perf_counter
+    rec = trace.append if trace is not None else (lambda e: None)
     me = _group_rank(group)
     total = len(owners)
     mine = sorted(units)
@@ -161,8 +211,10 @@ def compress_units(units: dict, owners: list[int], parallel: int, level: int, gr
                 units[h].speculate()
                 speculated.add(h)
             w.wait()
+            rec(("recv", g, clock()))
             entry, first = int(t[0]) & 0xFFFFFFFFFFFFFFFF, int(t[1])
         ex, nb = units[g].chain(entry, first)
+        rec(("chain", g, clock()))
         nblocks_local[g] = nb
         token = (ex, first + nb)
         if g + 1 < total and owners[g + 1] != me:
@@ -186,18 +238,29 @@ def compress_units(units: dict, owners: list[int], parallel: int, level: int, gr
         offs_l = [-1] * total
         crcb_l = [0] * total
         pieces = {}
-    for i, g in enumerate(mine):
+    if not local and seeds == "rounds":
+        idx = {g: i for i, g in enumerate(mine)}
+
+        def _enc(g, carried):
+            bits, crc = units[g].encode(carried)
+            rows[idx[g]] = (bits, crc & 0xFFFFFFFF, nblocks_local[g])
+            rec(("encode", g, clock()))
+
+        _seed_rounds(units, owners, mine, w, group, _enc, trace)
+    for i, g in enumerate(mine if (local or seeds != "rounds") else []):
         if g == 0:
             acc = np.zeros(w, dtype=np.uint32)
         elif owners[g - 1] != me:
             t = torch.zeros(w, dtype=torch.int32)
             dist.recv(t, src=owners[g - 1], group=group, tag=total + 1 + g)
+            rec(("sums", g, clock()))
             acc = t.numpy().view(np.uint32).copy()
         carried = acc.copy()
         acc = acc + units[g].sums().astype(np.uint32)   # uint32 wrap-around, as the reference's int array
         if g + 1 < total and owners[g + 1] != me:
             dist.send(torch.from_numpy(acc.view(np.int32).copy()), dst=owners[g + 1], group=group, tag=total + 2 + g)
         bits, crc = units[g].encode(carried)
+        rec(("encode", g, clock()))
         rows[i] = (bits, crc & 0xFFFFFFFF, nblocks_local[g])
         if local and nblocks_local[g] > 0:
             offs_l[g], crcb_l[g] = G, C

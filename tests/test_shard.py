@@ -395,3 +395,56 @@ def test_device_two_ranks_speculation():
             assert i["spliced"] == 0 or i["chained"] >= first, (g, i)
             merged += i["spliced"] > 0
     assert merged >= 1, info
+
+
+def _seed_worker(rank, world, port, q, seeds):
+    """The unit protocol on `world` gloo ranks with the seed sums exchanged by
+    all-gather rounds (or the stream-order token), units cut mid-run and
+    inside blocks; rank 0 reports equality with the single stream and every
+    rank its host timeline (chain token arrivals, rounds, encodes)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data = _stream_case(1_200_000, 0x5EED0606)
+    cuts = _cuts(len(data), 17, 10, 10000)
+    bufs = unit_buffers(data, cuts, bz2mi.unit_halo(1, 10000))
+    owners = shard.interleaved_owners(len(bufs), world)
+    units = {}
+    for g, (buf, n_own, n_halo, ends) in enumerate(bufs):
+        if owners[g] == rank:
+            u = CpuRefUnit(1, 3, 10000)
+            u.begin(buf, n_own, n_halo, ends)
+            units[g] = u
+    trace = []
+    lay = shard.compress_units(units, owners, 3, 1, seeds=seeds, trace=trace)
+    got = shard.gather_stream_host(lay, 1)
+    rounds = sum(1 for e in trace if e[0] == "round")
+    if rank == 0:
+        q.put((got == CpuRef().compress(data, 1, 3), len(bufs), rounds,
+               sum(1 for g in range(len(bufs)) if lay.nblocks[g] == 0)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("seeds", ["rounds", "token"])
+def test_gloo_four_ranks_seed_exchange(seeds):
+    """World 4: seed sums by one all-gather per round of units plus an
+    exclusive scan in stream order (SURVEY 8(e) exchange 1), and the token
+    alternative; p = 3 so every slot's running sum crosses ranks.  Equal to
+    the single-stream cpu_ref bytes; the rounds path takes ceil(units / 4)
+    collectives."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, world, port, q, seeds)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok, nunits, rounds, empty = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert ok
+    assert nunits >= 12 and empty >= 1, (nunits, empty)
+    assert rounds == (-(-nunits // world) if seeds == "rounds" else 0)
+    assert all(p.exitcode == 0 for p in procs)
