@@ -1032,8 +1032,10 @@ __device__ __forceinline__ uint32_t lds_emit_round(const uint8_t* __restrict__ T
         if (valid && !tie[e]) {
             const uint32_t i = src[e], pos = base + dst[e];
             if (s.sa) s.sa[pos] = i;
-            bwt[pos] = bwt_byte(T, n, i);
-            if (i == 0) *orig = pos;
+            if (bwt) {  // (null: the caller writes the BWT bytes from the final SA)
+                bwt[pos] = bwt_byte(T, n, i);
+                if (i == 0) *orig = pos;
+            }
         }
     }
     const uint32_t inc = wave_incl_sum(cnt);
@@ -3052,10 +3054,25 @@ __device__ __forceinline__ uint8_t text_owner(uint32_t run, uint32_t wk, uint32_
 }
 
 // a rotation's final position: its BWT byte (and origPtr)
+// BZ2MI_TEXT_FINALPASS (default): the BWT bytes and origPtr are written by
+// one coalesced pass over the finished SA at the end of the kernel instead of
+// a byte store per placed rotation (realtext BWT 46.3 -> 42.8 ms per GiB, A/B
+// on one box; write traffic unchanged at ~39 GB: the byte stores were not
+// where the writes are)
+#ifndef BZ2MI_TEXT_FINALPASS
+#define BZ2MI_TEXT_FINALPASS 1
+#endif
+// BZ2MI_TEXT_SCATTER2 (A/B, off): the pair scatter through a first-byte
+// order in the spill area; measured 42.8 -> 44.3 ms, writes 38.9 -> 40.7 GB
+#ifndef BZ2MI_TEXT_SCATTER2
+#define BZ2MI_TEXT_SCATTER2 0
+#endif
 __device__ __forceinline__ void text_final(const uint8_t* Tl, int n, uint32_t pos, uint32_t i, uint8_t* out,
                                            uint32_t* orig) {
-    out[pos] = bwt_byte(Tl, n, i);
-    if (i == 0) *orig = pos;
+    if (out) {  // (null under BZ2MI_TEXT_FINALPASS)
+        out[pos] = bwt_byte(Tl, n, i);
+        if (i == 0) *orig = pos;
+    }
 }
 
 // Deferred-group entries (a per-block list, capacity n / 2): start (17) |
@@ -3861,6 +3878,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
     const int n = (int)uniform(lens[b]);
     const uint8_t* T = blocks + (size_t)b * stride;
     uint8_t* out = bwt_out + (size_t)b * stride;
+    uint8_t* const bw = BZ2MI_TEXT_FINALPASS ? nullptr : out;  // BWT bytes written as rotations are placed
     uint32_t* orig = orig_out + b;
     uint32_t* sa = sa_all + (size_t)b * stride;
     uint32_t* spill = spill_all + (size_t)b * stride;
@@ -3990,9 +4008,27 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
     if (t == 0) atomicAdd(&g_tbk_x[11], wall_clock64() - tk0);
 #endif
-    // ---- every rotation to its pair bucket
+    // ---- every rotation to its pair bucket.  BZ2MI_TEXT_SCATTER2: through
+    // the first-byte order in `spill` (free until the sort phase): a 256-way
+    // scatter there (each bucket's append point is one L2 line, so the
+    // partial writes merge before they leave L2), then the pair scatter in
+    // that order, whose appends go to the pair buckets of one or two first
+    // bytes at a time -- instead of one 2,000-way scatter whose partial-line
+    // writes reached HBM one sector per rotation
+#if BZ2MI_TEXT_SCATTER2
+    if (t < 256) L.pcol[t] = L.cstart[t];
+    __syncthreads();
+    for (int i = t; i < n; i += FT) spill[atomicAdd(&L.pcol[Tl[i]], 1u)] = (uint32_t)i;
+    __threadfence_block();
+    __syncthreads();
+    for (int k = t; k < n; k += FT) {
+        const uint32_t i = ld_fresh(spill + k);
+        sa[atomicAdd(&cnt[pair_of(Tl[i], Tl[i + 1 < (uint32_t)n ? i + 1 : 0])], 1u)] = i;
+    }
+#else
     for (int i = t; i < n; i += FT)
         sa[atomicAdd(&cnt[pair_of(Tl[i], Tl[i + 1 < n ? i + 1 : 0])], 1u)] = (uint32_t)i;
+#endif
     __threadfence_block();
     __syncthreads();
 #ifdef BZ2MI_PHASES
@@ -4023,7 +4059,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
         uint32_t bst = 0, blen = 0, bcnt = 0;
         auto flush = [&]() {
             if (blen >= 2) dl2[atomicAdd(&L.nitems, 1u)] = tq_item(bst, blen, bcnt > 1 ? 1u : 2u);
-            else if (blen == 1) text_final(Tl, n, bst, ld_fresh(sa + bst), out, orig);
+            else if (blen == 1) text_final(Tl, n, bst, ld_fresh(sa + bst), bw, orig);
             blen = bcnt = 0;
         };
         for (uint32_t wq = 0; wq < 8; ++wq) {
@@ -4109,8 +4145,8 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
         const unsigned long long ti0 = wall_clock64();
 #endif
-        if (seg.len <= (uint32_t)kTS) text_sort(Tl, n, sa, seg, d, out, orig, W, L, dl);
-        else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, kWqPush);
+        if (seg.len <= (uint32_t)kTS) text_sort(Tl, n, sa, seg, d, bw, orig, W, L, dl);
+        else text_partition(Tl, n, sa, spill, seg, d, bw, orig, W, L, kWqPush);
         TBK_T(11, seg.len);
 #ifdef BZ2MI_PHASES
         TBK_COUNT(seg.len <= (uint32_t)kTS ? 12 : 13, wall_clock64() - ti0);
@@ -4170,8 +4206,8 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
             const unsigned long long ti0 = wall_clock64();
 #endif
-            if (seg.len <= (uint32_t)kTS) text_sort_pre(Tl, n, sa, seg, d, out, orig, W, L, dl, pre);
-            else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, 0);
+            if (seg.len <= (uint32_t)kTS) text_sort_pre(Tl, n, sa, seg, d, bw, orig, W, L, dl, pre);
+            else text_partition(Tl, n, sa, spill, seg, d, bw, orig, W, L, 0);
             TBK_T(10, seg.len);
 #ifdef BZ2MI_PHASES
             TBK_COUNT(seg.len <= (uint32_t)kTS ? 12 : 13, wall_clock64() - ti0);
@@ -4224,8 +4260,8 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
             const unsigned long long ti0 = wall_clock64();
 #endif
-            if (seg.len <= (uint32_t)kTS) text_sort(Tl, n, sa, seg, d, out, orig, W, L, dl);
-            else text_partition(Tl, n, sa, spill, seg, d, out, orig, W, L, cur ^ 1);
+            if (seg.len <= (uint32_t)kTS) text_sort(Tl, n, sa, seg, d, bw, orig, W, L, dl);
+            else text_partition(Tl, n, sa, spill, seg, d, bw, orig, W, L, cur ^ 1);
             TBK_T(11, seg.len);
 #ifdef BZ2MI_PHASES
             TBK_COUNT(seg.len <= (uint32_t)kTS ? 12 : 13, wall_clock64() - ti0);
@@ -4291,7 +4327,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #ifdef BZ2MI_PHASES
         if (t == 0) atomicAdd(&g_tbk_res[0], wall_clock64() - tkr);
 #endif
-        text_resolve_all(Tl, n, sa, isa, dl, ndef, dl2, out, orig, L);
+        text_resolve_all(Tl, n, sa, isa, dl, ndef, dl2, bw, orig, L);
         __threadfence_block();
         __syncthreads();
     }
@@ -4337,7 +4373,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                 if (tgt) {
                     const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
                     sa[bs + below] = j;
-                    text_final(Tl, n, bs + below, j, out, orig);
+                    text_final(Tl, n, bs + below, j, bw, orig);
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (tgt && (peers & __lanemask_lt()) == 0) C[x] = bs + (uint32_t)__popcll(peers);
@@ -4422,7 +4458,7 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
                         const uint32_t below = (uint32_t)__popcll(peers & __lanemask_lt());
                         const uint32_t pos = bs + below;
                         sa[pos] = jv[r];
-                        text_final(Tl, n, pos, jv[r], out, orig);
+                        text_final(Tl, n, pos, jv[r], bw, orig);
                         if (below == 0) C[x] = bs + (uint32_t)__popcll(peers);
                     }
                     __builtin_amdgcn_wave_barrier();
@@ -4436,6 +4472,31 @@ __global__ __launch_bounds__(FT) void bwt_text_kernel(const uint8_t* __restrict_
 #endif
     }
     __syncthreads();
+#if BZ2MI_TEXT_FINALPASS
+    if (!uniform(L.fail)) {
+        // BWT bytes and origPtr from the finished SA, 4 positions per thread:
+        // a 16-byte SA load and a 4-byte store
+        for (uint32_t k0 = 4u * (uint32_t)t; k0 < (uint32_t)n; k0 += 4u * FT) {
+            if (k0 + 4u <= (uint32_t)n) {
+                const uint4 v = *reinterpret_cast<const uint4*>(sa + k0);
+                const uint32_t ii[4] = {v.x & 0x1ffffu, v.y & 0x1ffffu, v.z & 0x1ffffu, v.w & 0x1ffffu};
+                uint32_t word = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    word |= (uint32_t)bwt_byte(Tl, n, ii[j]) << (8 * j);
+                    if (ii[j] == 0) *orig = k0 + (uint32_t)j;
+                }
+                *reinterpret_cast<uint32_t*>(out + k0) = word;
+            } else {
+                for (uint32_t k = k0; k < (uint32_t)n; ++k) {
+                    const uint32_t i = ld_fresh(sa + k) & 0x1ffffu;
+                    out[k] = bwt_byte(Tl, n, i);
+                    if (i == 0) *orig = k;
+                }
+            }
+        }
+    }
+#endif
     if (t == 0 && L.fail) redo[b] = 2u;
     TBK_T(6, L.fail);
 #ifdef BZ2MI_PHASES
