@@ -99,6 +99,8 @@ struct bz2mi_dctx {
     size_t merged_cap = 0;
     uint32_t* d_marks = nullptr;
     size_t marks_cap = 0;
+    uint8_t* d_iscr = nullptr;  // inverse-BWT walker bytes (kDecIbwtScratch per workgroup of its grid)
+    size_t iscr_cap = 0;
     uint8_t* d_rle1 = nullptr;
     size_t rle1_cap = 0;
     uint32_t* d_cstate = nullptr;
@@ -420,6 +422,8 @@ int run_window(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint64_t start, boo
         if ((r = grow(&d->d_blocks, &d->blocks_cap, nb))) return r;
         if ((r = grow(&d->d_merged, &d->merged_cap, std::max(nb * stride, nb * sym_stride)))) return r;
         if ((r = grow(&d->d_marks, &d->marks_cap, nb * stride))) return r;
+        const size_t ibwt_grid = std::min<size_t>(nb, (size_t)8 * ibwt_wg_per_xcd());
+        if ((r = grow(&d->d_iscr, &d->iscr_cap, ibwt_grid * kDecIbwtScratch))) return r;
         if ((r = grow(&d->d_rle1, &d->rle1_cap, nb * stride))) return r;
         if ((r = grow(&d->d_cstate, &d->cstate_cap, nb * 256))) return r;
         if ((r = grow(&d->d_olen, &d->olen_cap, nb))) return r;
@@ -428,9 +432,9 @@ int run_window(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint64_t start, boo
         if ((r = grow(&d->d_bad, &d->bad_cap, nb))) return r;
         DCHECK(hipMemsetAsync(d->d_bad, 0, nb * sizeof(uint32_t), s));
         DCHECK(hipMemcpyAsync(d->d_blocks, chain.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(dec_ibwt_kernel, dim3((unsigned)std::min<size_t>(nb, (size_t)8 * ibwt_wg_per_xcd())),
-                           dim3(kDecIbwtThreads), 0, s, d->d_bwt, stride, d->d_info, d->d_blocks, (uint32_t)nb,
-                           d->d_merged, stride, d->d_marks, stride, d->d_rle1, stride, d->d_bad);
+        hipLaunchKernelGGL(dec_ibwt_kernel, dim3((unsigned)ibwt_grid), dim3(kDecIbwtThreads), 0, s, d->d_bwt, stride,
+                           d->d_info, d->d_blocks, (uint32_t)nb, d->d_merged, stride, d->d_marks, stride, d->d_rle1,
+                           stride, d->d_bad, d->d_iscr);
         DCHECK(hipGetLastError());
         DCHECK(hipEventRecord(d->ev[4], s));
         hipLaunchKernelGGL(dec_rle1_kernel, dim3((unsigned)nb), dim3(256), 0, s, d->d_rle1, stride, d->d_info,
@@ -656,7 +660,7 @@ void bz2mi_ddestroy(bz2mi_dctx* d) {
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     for (void* p : {(void*)d->d_crctab, (void*)d->d_cnt, (void*)d->d_cand, (void*)d->d_ids, (void*)d->d_bwt,
                     (void*)d->d_syms, (void*)d->d_symmap, (void*)d->d_tabs, (void*)d->d_info, (void*)d->d_blocks, (void*)d->d_merged,
-                    (void*)d->d_marks, (void*)d->d_rle1, (void*)d->d_cstate, (void*)d->d_olen, (void*)d->d_ooff,
+                    (void*)d->d_marks, (void*)d->d_iscr, (void*)d->d_rle1, (void*)d->d_cstate, (void*)d->d_olen, (void*)d->d_ooff,
                     (void*)d->d_crc, (void*)d->d_in, (void*)d->d_out, (void*)d->d_bad})
         if (p) (void)hipFree(p);
     for (auto& e : d->ev)

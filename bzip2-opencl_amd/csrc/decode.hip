@@ -728,12 +728,28 @@ constexpr int kWPT = 8;               // walkers per thread
 constexpr int kWalkers = kIT * kWPT;  // per block
 constexpr uint16_t kEnd = 0xffff;
 static_assert(kWalkers <= 0xffff, "walker ids fit 16 bits");
+// BZ2MI_IBWT_ONEWALK (default): one walk of the LF cycle instead of two --
+// every walker keeps its segment's bytes (8 in registers, stored 8 at a
+// time to its kWCap-byte area of the workgroup's scratch) while it measures
+// the segment, and once the segments are chained the bytes are copied to
+// their offsets; only the bytes of a segment beyond kWCap (mean length n /
+// 8192 ~ 11: about 1 segment in 10^5 at S = 90,000) are walked a second time.
+// The walks are random 4-byte loads from the merged vector (a 64-byte line
+// each): one walk halves them.
+#ifndef BZ2MI_IBWT_ONEWALK
+#define BZ2MI_IBWT_ONEWALK 1
+#endif
+constexpr uint32_t kWCap = 128;
+static_assert((size_t)kWalkers * kWCap == kDecIbwtScratch, "walker scratch layout");
 
 struct IbwtLds {
     uint32_t base[kIW][256];   // per-wave byte counts -> merged-vector bases
     uint32_t seglen[kWalkers];
     uint32_t sfx[kWalkers];    // suffix sums of segment lengths along the chain
     uint16_t nxt[kWalkers];    // successor segment (pointer jumping), kEnd past the last
+#if BZ2MI_IBWT_ONEWALK
+    uint32_t resume[kWalkers]; // row of byte kWCap of a segment longer than kWCap
+#endif
     uint32_t tmp[kIW];
     uint32_t period;
 };
@@ -742,7 +758,7 @@ __device__ __forceinline__ void ibwt_one(IbwtLds& L, uint32_t bi, const uint8_t*
                                          const DecBlockInfo* __restrict__ infos, const uint32_t* __restrict__ blocks,
                                          uint32_t* __restrict__ merged, size_t mstride, uint32_t* __restrict__ marks,
                                          size_t kstride, uint8_t* __restrict__ rle1, size_t rstride,
-                                         uint32_t* __restrict__ bad_out) {
+                                         uint32_t* __restrict__ bad_out, uint8_t* __restrict__ ws) {
     const uint32_t k = blocks[bi];  // decoded-candidate index
     const int t = threadIdx.x, w = wave_id(), lane = lane_id();
     const uint32_t n = infos[k].len;
@@ -820,6 +836,69 @@ __device__ __forceinline__ void ibwt_one(IbwtLds& L, uint32_t bi, const uint8_t*
     // loads of all the thread's walkers are issued together
     uint32_t x[kWPT], len[kWPT], m[kWPT];
     bool act[kWPT];
+#if BZ2MI_IBWT_ONEWALK
+    uint32_t bw[kWPT][2];  // the segment's pending bytes (8), stored 8 at a time
+#pragma unroll
+    for (int q = 0; q < kWPT; ++q) {
+        const int j = t + kIT * q;
+        act[q] = is_start(j);
+        x[q] = start_of(j);
+        len[q] = 0;
+        m[q] = act[q] ? M[x[q]] : 0u;
+        bw[q][0] = bw[q][1] = 0;
+    }
+    {
+        bool any1 = true;
+        while (any1) {
+            uint32_t nx[kWPT], mv[kWPT];
+#pragma unroll
+            for (int q = 0; q < kWPT; ++q) {
+                nx[q] = (m[q] & 0x7fffffffu) >> 8;
+                if (act[q] && (nx[q] >= n || len[q] >= n)) {  // inconsistent data (never for valid blocks)
+                    act[q] = false;
+                    if (bad) *bad = 1u;
+                }
+                if (act[q] && len[q] < kWCap) {
+                    // byte len of the segment: the row's own byte
+                    const uint32_t kb = len[q], by = m[q] & 255u, sh = 8u * (kb & 3u);
+                    const bool hi = (kb & 4u) != 0;
+                    bw[q][0] |= hi ? 0u : by << sh;
+                    bw[q][1] |= hi ? by << sh : 0u;
+                    if ((kb & 7u) == 7u) {
+                        *reinterpret_cast<uint2*>(ws + (size_t)(t + kIT * q) * kWCap + (kb & ~7u)) =
+                            make_uint2(bw[q][0], bw[q][1]);
+                        bw[q][0] = bw[q][1] = 0;
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kWPT; ++q) mv[q] = act[q] ? M[nx[q]] : 0u;
+            any1 = false;
+#pragma unroll
+            for (int q = 0; q < kWPT; ++q) {
+                if (!act[q]) continue;
+                const int j = t + kIT * q;
+                len[q]++;
+                x[q] = nx[q];
+                m[q] = mv[q];
+                if (len[q] == kWCap) L.resume[j] = x[q];
+                if (m[q] >> 31) {
+                    act[q] = false;
+                    L.seglen[j] = len[q];
+                    if (len[q] < kWCap && (len[q] & 7u))  // the last partial 8
+                        *reinterpret_cast<uint2*>(ws + (size_t)j * kWCap + (len[q] & ~7u)) =
+                            make_uint2(bw[q][0], bw[q][1]);
+                    const uint32_t sj = mark[x[q]];
+                    L.nxt[j] = sj == 0 ? kEnd : (uint16_t)sj;
+                } else {
+                    any1 = true;
+                }
+            }
+        }
+    }
+    if (false)
+#endif
+    {
 #pragma unroll
     for (int q = 0; q < kWPT; ++q) {
         const int j = t + kIT * q;
@@ -859,6 +938,7 @@ __device__ __forceinline__ void ibwt_one(IbwtLds& L, uint32_t bi, const uint8_t*
             }
         }
     }
+    }
     __syncthreads();
     // chain the segments of origPtr's cycle by pointer jumping: sfx[j] = the
     // lengths from segment j to the chain's last; a segment's offset is
@@ -896,6 +976,31 @@ __device__ __forceinline__ void ibwt_one(IbwtLds& L, uint32_t bi, const uint8_t*
     const uint32_t per = L.period;
     // pass B: write the bytes of each segment
     uint32_t o[kWPT];
+#if BZ2MI_IBWT_ONEWALK
+    // the kept bytes to their offsets; segments longer than kWCap walk on
+    // from their resume row for the rest
+#pragma unroll
+    for (int q = 0; q < kWPT; ++q) {
+        const int j = t + kIT * q;
+        const uint32_t sl = L.seglen[j], sf = L.sfx[j];
+        const bool placed = is_start(j) && L.nxt[j] == kEnd && sf <= per && sl > 0;
+        o[q] = placed ? per - sf : 0u;
+        const uint32_t keep = placed ? min(sl, kWCap) : 0u;
+        const uint8_t* src = ws + (size_t)j * kWCap;
+        for (uint32_t c0 = 0; c0 < keep; c0 += 16) {
+            const uint4 v = *reinterpret_cast<const uint4*>(src + c0);
+            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int b = 0; b < 16; ++b)
+                if (c0 + (uint32_t)b < keep) out[o[q] + c0 + (uint32_t)b] = (uint8_t)(vv[b >> 2] >> (8 * (b & 3)));
+        }
+        len[q] = placed && sl > kWCap ? sl - kWCap : 0u;
+        x[q] = len[q] ? L.resume[j] : 0u;
+        o[q] += kWCap;
+    }
+    if (false)
+#endif
+    {
 #pragma unroll
     for (int q = 0; q < kWPT; ++q) {
         const int j = t + kIT * q;
@@ -906,7 +1011,8 @@ __device__ __forceinline__ void ibwt_one(IbwtLds& L, uint32_t bi, const uint8_t*
         len[q] = placed ? sl : 0u;
         o[q] = placed ? per - sf : 0u;
     }
-    any = true;
+    }
+    bool any = true;
     while (any) {
         uint32_t mv[kWPT];
 #pragma unroll
@@ -941,10 +1047,12 @@ __global__ __launch_bounds__(kIT) void dec_ibwt_kernel(const uint8_t* __restrict
                                                        uint32_t* __restrict__ merged, size_t mstride,
                                                        uint32_t* __restrict__ marks, size_t kstride,
                                                        uint8_t* __restrict__ rle1, size_t rstride,
-                                                       uint32_t* __restrict__ bad_out) {
+                                                       uint32_t* __restrict__ bad_out, uint8_t* __restrict__ wscr) {
     __shared__ IbwtLds L;
+    // (wscr: kWalkers * kWCap bytes per workgroup of the grid)
+    uint8_t* ws = wscr + (size_t)blockIdx.x * ((size_t)kWalkers * kWCap);
     for (uint32_t bi = blockIdx.x; bi < nblocks; bi += gridDim.x) {
-        ibwt_one(L, bi, bwt, stride, infos, blocks, merged, mstride, marks, kstride, rle1, rstride, bad_out);
+        ibwt_one(L, bi, bwt, stride, infos, blocks, merged, mstride, marks, kstride, rle1, rstride, bad_out, ws);
         __syncthreads();
     }
 }

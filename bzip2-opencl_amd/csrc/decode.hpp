@@ -55,6 +55,7 @@ __global__ void dec_huff_kernel(const uint8_t* in, uint64_t n, const DecCand* ca
 #endif
 constexpr int kDecSymBlocks = BZ2MI_SYM_BLOCKS;  // blocks per wave of dec_sym_kernel
 constexpr int kDecIbwtThreads = 1024;             // threads per dec_ibwt_kernel workgroup
+constexpr size_t kDecIbwtScratch = (size_t)kDecIbwtThreads * 8 * 128;  // walker bytes per dec_ibwt_kernel workgroup
 // symbol row j <- candidate sel[j]
 __global__ void dec_sym_kernel(const uint8_t* in, uint64_t n, const uint8_t* tabs, const uint32_t* sel, uint32_t nids,
                                uint32_t smax, uint16_t* syms, size_t sym_stride, DecBlockInfo* infos);
@@ -64,7 +65,8 @@ __global__ void dec_mtf_kernel(const uint16_t* syms, size_t sym_stride, const ui
                                uint32_t* scratch, size_t sstride, uint8_t* bwt, size_t stride, DecBlockInfo* infos);
 __global__ void dec_ibwt_kernel(const uint8_t* bwt, size_t stride, const DecBlockInfo* infos,
                                 const uint32_t* blocks, uint32_t nblocks, uint32_t* merged, size_t mstride,
-                                uint32_t* marks, size_t kstride, uint8_t* rle1, size_t rstride, uint32_t* bad);
+                                uint32_t* marks, size_t kstride, uint8_t* rle1, size_t rstride, uint32_t* bad,
+                                uint8_t* wscr);
 __global__ void dec_rle1_kernel(const uint8_t* rle1, size_t rstride, const DecBlockInfo* infos,
                                 const uint32_t* blocks, uint32_t nblocks, uint32_t* chunk_state, uint64_t* out_len,
                                 const uint64_t* out_off, uint8_t* out, uint64_t cap, uint32_t* crc_out,
