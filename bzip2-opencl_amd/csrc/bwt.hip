@@ -967,6 +967,7 @@ struct Bucket3Lds {
     static constexpr bool kKeys = false;
     uint32_t base[257];
     uint32_t idx[kSmall];
+    uint8_t sbyte[kSmall];  // the sub-bucket byte of every position (read in order by the counting phase)
 };
 
 template <class BL>
@@ -1321,6 +1322,7 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
             if ((uint32_t)(e * 64 + lane) < seg.len) {
                 const uint32_t pos = L.base[key[e] >> 56] + slot[e];
                 if constexpr (BL::kKeys) L.key[pos] = key[e];
+                else L.sbyte[pos] = (uint8_t)(key[e] >> 56);
                 L.idx[pos] = ii[e];
             }
         }
@@ -1379,9 +1381,8 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
         auto elem_state = [&](int e, uint32_t& w, uint32_t& bm) {
             const uint32_t p = (uint32_t)(e * 64 + lane);
             w = p < seg.len ? L.idx[p] : 0u;
-            uint32_t pc = (w & 0x1ffffu) + d;
-            if (pc >= (uint32_t)n) pc %= (uint32_t)n;
-            const uint32_t c = p < seg.len ? (uint32_t)T[pc] : 0u;
+            // (the sub-bucket byte from its in-order copy, not a random read of the LDS text)
+            const uint32_t c = p < seg.len ? (uint32_t)L.sbyte[p] : 0u;
             const uint32_t b0 = L.base[c], m = L.base[c + 1] - b0;
             bm = p < seg.len && m <= (uint32_t)kSub ? b0 | (m << 9) : 0u;
         };
