@@ -258,9 +258,9 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
                            t.d_bwt, t.d_orig, c->d_sq, scount, scap, c->d_lq[1], lcount + kBwtShards, lcap,
                            t.d_present, c->d_tq[1], tc[1], tcap);
         HIPCHECK(hipGetLastError());
-        hipLaunchKernelGGL(bwt_bigbucket_kernel, dim3(256, nb), dim3(kBigBucketThreads), 0, s, t.d_blocks, c->stride, t.d_lens,
-                           t.d_sa, t.d_bwt, t.d_orig, c->d_tq[1], tc[1], tcap, c->d_tq[0], tc[0], tcap, c->d_lq[0],
-                           lcount + 2 * kBwtShards, lcap);
+        hipLaunchKernelGGL(bwt_bigbucket_kernel, bigbucket_grid(nb), dim3(kBigBucketThreads), 0, s, t.d_blocks, c->stride,
+                           t.d_lens, t.d_sa, t.d_bwt, t.d_orig, c->d_tq[1], tc[1], tcap, c->d_tq[0], tc[0], tcap,
+                           c->d_lq[0], lcount + 2 * kBwtShards, lcap, nb);
     }
     HIPCHECK(hipGetLastError());
     STAGE_DONE("bwt_bucket");
@@ -328,7 +328,18 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
             fprintf(stderr, "[bz2mi] doubling: %u blocks\n", np);
         }
     } else {
-        // grid-wide doubling: every launch returns at once when nothing is left
+        // grid-wide doubling: every launch returns at once when nothing is left;
+        // when no block has groups left after the tie rounds (random-like
+        // data) its ~100 launches are skipped (one count read back instead)
+        {
+            uint32_t np = 0;
+            HIPCHECK(hipMemcpyAsync(&np, p2count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            if (np == 0) {
+                STAGE_DONE("bwt");
+                return BZ2MI_OK;
+            }
+        }
         DblGrid G{t.d_blocks, c->stride, t.d_lens, t.d_sa, t.d_bwt, t.d_orig, t.d_groups, t.d_ngroups, t.d_p2list,
                   p2count, c->d_dscratch, dbl_slot_bytes(c->S), c->S, {c->d_dlist[0], c->d_dlist[1]},
                   {c->d_dlarge[0], c->d_dlarge[1]}, c->d_dctr};

@@ -2083,6 +2083,8 @@ struct BigLds {
     uint32_t base[257];
     uint32_t tmp[16];
 };
+// (BZ2MI_BIG_XCD, kernels.hpp: the big-bucket grid dealt to the XCDs by block;
+// A/B -DBZ2MI_BIG_XCD=0 = the block-major 2-D grid)
 // threads per big-bucket workgroup (A/B: -DBZ2MI_BIG_NT=256)
 #ifndef BZ2MI_BIG_NT
 #define BZ2MI_BIG_NT 512
@@ -2097,13 +2099,24 @@ __global__ __launch_bounds__(kBigNT) void bwt_bigbucket_kernel(const uint8_t* __
                                                             const uint32_t* __restrict__ bq_count, size_t bq_cap,
                                                             uint64_t* __restrict__ tl, uint32_t* __restrict__ tcount,
                                                             size_t tcap, BwtItem* __restrict__ lq,
-                                                            uint32_t* __restrict__ lcount, size_t lcap) {
+                                                            uint32_t* __restrict__ lcount, size_t lcap, int nblocks) {
     __shared__ BigLds L;
+#if BZ2MI_BIG_XCD
+    // 1-D grid of 8 x 256 x ceil(blocks / 8): the dispatcher deals workgroup
+    // w to XCD w mod 8, so XCD x takes the blocks b = x (mod 8), the 256
+    // buckets of one block after another -- a block's text is fetched into
+    // one XCD's L2 once and its few concurrent blocks stay there
+    const uint32_t xcd = blockIdx.x & 7u, sl = blockIdx.x >> 3;
+    const uint32_t b = (sl >> 8) * 8u + xcd, bk = sl & 255u;
+    if (b >= (uint32_t)nblocks) return;
+#else
     // grid (256, blocks): consecutive workgroups share a block, so the
     // concurrent ones gather from a few blocks' text (L2-resident), not all
-    const uint32_t b = blockIdx.y;
-    if (blockIdx.x >= bq_count[b]) return;
-    const uint64_t e = bq[(size_t)b * bq_cap + blockIdx.x];
+    const uint32_t b = blockIdx.y, bk = blockIdx.x;
+    (void)nblocks;
+#endif
+    if (bk >= bq_count[b]) return;
+    const uint64_t e = bq[(size_t)b * bq_cap + bk];
     const uint32_t start = (uint32_t)(e >> 32), len = (uint32_t)e;
     const int n = (int)lens[b];
     const uint8_t* T = blocks + (size_t)b * stride;

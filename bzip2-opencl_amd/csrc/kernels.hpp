@@ -29,16 +29,26 @@ __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const ui
                                   uint32_t* scount, size_t scap, BwtItem* lq, uint32_t* lcount, size_t lcap,
                                   uint32_t* present_out, uint64_t* bq, uint32_t* bq_count, size_t bq_cap);
 // buckets of 512 < c <= 4096 rotations listed by bwt_bucket_kernel in bq (per
-// block, bq_cap entries, count bq_count[b]): grid (256, blocks) of
+// block, bq_cap entries, count bq_count[b]): bigbucket_grid(blocks) of
 // kBigBucketThreads
 #ifndef BZ2MI_BIG_NT
 #define BZ2MI_BIG_NT 512
 #endif
+#ifndef BZ2MI_BIG_XCD
+#define BZ2MI_BIG_XCD 1
+#endif
 constexpr int kBigBucketThreads = BZ2MI_BIG_NT;
+inline dim3 bigbucket_grid(int nblocks) {
+#if BZ2MI_BIG_XCD
+    return dim3(8u * 256u * (((unsigned)nblocks + 7u) / 8u));
+#else
+    return dim3(256, nblocks);
+#endif
+}
 __global__ void bwt_bigbucket_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                      uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* bq,
                                      const uint32_t* bq_count, size_t bq_cap, uint64_t* tl, uint32_t* tcount,
-                                     size_t tcap, BwtItem* lq, uint32_t* lcount, size_t lcap);
+                                     size_t tcap, BwtItem* lq, uint32_t* lcount, size_t lcap, int nblocks);
 // Blocks of <= kBwtLdsText bytes: the first-byte sort and the sort of the
 // small buckets in one launch, the block's text held in LDS (1024 threads, one
 // workgroup per CU).  Large buckets still go to the level queue.
