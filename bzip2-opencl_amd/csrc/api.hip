@@ -307,12 +307,13 @@ int stage_bwt(bz2mi_ctx* c, Batch& t, int nb, hipStream_t s) {
     // doubling resolves long repeated passages directly)
     // (big blocks: 8 workgroups per block, each a slice of its list)
     const int tie_rounds = blk ? kBwtTieRounds : kBwtTieRoundsGrid;
-    const unsigned tie_split = blk ? 1u : 8u;
     for (int r = 0; r < tie_rounds; ++r) {
         HIPCHECK(hipMemsetAsync(tc[(r + 1) & 1], 0, nb * sizeof(uint32_t), s));
-        hipLaunchKernelGGL(bwt_tie_kernel, dim3(nb, tie_split), dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, t.d_sa,
+        // (900 KB blocks: 8 slices per block, dealt to the XCDs by block)
+        const dim3 tgrid = blk ? dim3(nb, 1) : dim3(8u * (unsigned)kTieSlices * (((unsigned)nb + 7u) / 8u));
+        hipLaunchKernelGGL(bwt_tie_kernel, tgrid, dim3(256), 0, s, t.d_blocks, c->stride, t.d_lens, t.d_sa,
                            t.d_bwt, t.d_orig, c->d_tq[r & 1], tc[r & 1], c->d_tq[(r + 1) & 1], tc[(r + 1) & 1], tcap,
-                           t.d_groups, t.d_ngroups, t.d_p2list, p2count, r + 1 == tie_rounds ? 1 : 0);
+                           t.d_groups, t.d_ngroups, t.d_p2list, p2count, r + 1 == tie_rounds ? 1 : 0, nb, blk ? 0 : 1);
         HIPCHECK(hipGetLastError());
     }
     STAGE_DONE("bwt_ties");

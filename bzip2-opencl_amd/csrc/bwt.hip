@@ -4559,11 +4559,28 @@ __global__ __launch_bounds__(256) void bwt_tie_kernel(const uint8_t* __restrict_
                                                       uint64_t* __restrict__ tout, uint32_t* __restrict__ tout_count,
                                                       size_t tcap, Seg* __restrict__ grp_all,
                                                       uint32_t* __restrict__ ngroups, uint32_t* __restrict__ p2list,
-                                                      uint32_t* __restrict__ p2count, int last) {
+                                                      uint32_t* __restrict__ p2count, int last, int nblocks,
+                                                      int xcd_map) {
     __shared__ TieLds L;
-    const uint32_t b = blockIdx.x;
+    // xcd_map (900 KB blocks): a 1-D grid of 64 x ceil(blocks / 8) where XCD
+    // x (workgroup w -> XCD w mod 8) takes the blocks b = x (mod 8), the 8
+    // slices of one block after another, so the blocks in flight (whose text
+    // the members gather from) are a few per XCD instead of every block of
+    // the batch; else grid (blocks, slices)
+    uint32_t b, ysl, nsl;
+    if (xcd_map) {
+        const uint32_t xcd = blockIdx.x & 7u, sl = blockIdx.x >> 3;
+        b = (sl / (uint32_t)kTieSlices) * 8u + xcd;
+        ysl = sl % (uint32_t)kTieSlices;
+        nsl = (uint32_t)kTieSlices;
+        if (b >= (uint32_t)nblocks) return;
+    } else {
+        b = blockIdx.x;
+        ysl = blockIdx.y;
+        nsl = gridDim.y;
+    }
     const uint32_t nq = uniform(tin_count[b]);
-    const uint32_t y0 = blockIdx.y * NT, ystep = gridDim.y * NT;
+    const uint32_t y0 = ysl * NT, ystep = nsl * NT;
     if (y0 >= nq) return;
     const int n = (int)uniform(lens[b]);
     const uint8_t* T = blocks + (size_t)b * stride;

@@ -38,6 +38,11 @@ __global__ void bwt_bucket_kernel(const uint8_t* blocks, size_t stride, const ui
 #define BZ2MI_BIG_XCD 1
 #endif
 constexpr int kBigBucketThreads = BZ2MI_BIG_NT;
+// workgroups per 900 KB block of a tie round (A/B: -DBZ2MI_TIE_SLICES=n)
+#ifndef BZ2MI_TIE_SLICES
+#define BZ2MI_TIE_SLICES 8
+#endif
+constexpr int kTieSlices = BZ2MI_TIE_SLICES;
 inline dim3 bigbucket_grid(int nblocks) {
 #if BZ2MI_BIG_XCD
     return dim3(8u * 256u * (((unsigned)nblocks + 7u) / 8u));
@@ -100,7 +105,7 @@ constexpr int kBwtTieRoundsGrid = BZ2MI_AB_TIE_ROUNDS_GRID;  // ... before the g
 __global__ void bwt_tie_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, uint32_t* sa_all,
                                uint8_t* bwt_out, uint32_t* orig_out, const uint64_t* tin, const uint32_t* tin_count,
                                uint64_t* tout, uint32_t* tout_count, size_t tcap, BwtSeg* grp_all,
-                               uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count, int last);
+                               uint32_t* ngroups, uint32_t* p2list, uint32_t* p2count, int last, int nblocks, int xcd_map);
 constexpr int kBwtShards = 64;  // queue shards (bwt.hip kShards)
 __global__ void bwt_double_kernel(const uint8_t* blocks, size_t stride, const uint32_t* lens, int nblocks,
                                   uint32_t* sa_all, uint8_t* bwt_out, uint32_t* orig_out, uint8_t* scratch,
