@@ -967,7 +967,6 @@ struct Bucket3Lds {
     static constexpr bool kKeys = false;
     uint32_t base[257];
     uint32_t idx[kSmall];
-    uint8_t sbyte[kSmall];  // the sub-bucket byte of every position (read in order by the counting phase)
 };
 
 template <class BL>
@@ -1279,6 +1278,10 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
 #endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) L.base[lane * 4 + j] = 0;
+    // LDS text: every element's own state for the counting phase, kept in
+    // registers from the scatter (word; sub-bucket start | size << 9 | its
+    // slot in it << 20, 0 when not a small sub-bucket) -- no LDS reads of it
+    uint32_t own_w[E], own_sb[E];
     {
         uint32_t ii[E], slot[E];
         uint64_t key[E];
@@ -1319,10 +1322,18 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
         }
 #pragma unroll
         for (int e = 0; e < E; ++e) {
+            own_w[e] = ii[e];
+            own_sb[e] = 0;
             if ((uint32_t)(e * 64 + lane) < seg.len) {
-                const uint32_t pos = L.base[key[e] >> 56] + slot[e];
-                if constexpr (BL::kKeys) L.key[pos] = key[e];
-                else L.sbyte[pos] = (uint8_t)(key[e] >> 56);
+                const uint32_t c = (uint32_t)(key[e] >> 56);
+                const uint32_t b0 = L.base[c];
+                const uint32_t pos = b0 + slot[e];
+                if constexpr (BL::kKeys) {
+                    L.key[pos] = key[e];
+                } else {
+                    const uint32_t m = L.base[c + 1] - b0;
+                    own_sb[e] = m <= (uint32_t)kSub ? b0 | (m << 9) | (slot[e] << 20) : 0u;
+                }
                 L.idx[pos] = ii[e];
             }
         }
@@ -1381,24 +1392,29 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
         auto elem_state = [&](int e, uint32_t& w, uint32_t& bm) {
             const uint32_t p = (uint32_t)(e * 64 + lane);
             w = p < seg.len ? L.idx[p] : 0u;
-            // (the sub-bucket byte from its in-order copy, not a random read of the LDS text)
-            const uint32_t c = p < seg.len ? (uint32_t)L.sbyte[p] : 0u;
+            uint32_t pc = (w & 0x1ffffu) + d;
+            if (pc >= (uint32_t)n) pc %= (uint32_t)n;
+            const uint32_t c = p < seg.len ? (uint32_t)T[pc] : 0u;
             const uint32_t b0 = L.base[c], m = L.base[c + 1] - b0;
             bm = p < seg.len && m <= (uint32_t)kSub ? b0 | (m << 9) : 0u;
         };
         uint32_t iw[E], sb[E];  // word; b0 | m << 9 (m = 0: not a small sub-bucket of this segment)
 #if BZ2MI_CNT_INTERLEAVE
-        // every element's state first, then the member loops of all E
-        // elements interleaved: trip q reads member q of each element's
-        // sub-bucket (E independent LDS reads in flight per trip, trips = the
-        // largest sub-bucket instead of the sum over the elements)
+        // every element's state (kept from the scatter: the elements are
+        // taken in their original order, not by position), then the member
+        // loops of all E elements interleaved: trip q reads member q of each
+        // element's sub-bucket (E independent LDS reads in flight per trip,
+        // trips = the largest sub-bucket instead of the sum over the elements)
 #pragma unroll
-        for (int e = 0; e < E; ++e) elem_state(e, iw[e], sb[e]);
+        for (int e = 0; e < E; ++e) {
+            iw[e] = own_w[e];
+            sb[e] = own_sb[e];
+        }
         // per element: lt | le << 16 (counts < 512), and one tie bit each
         uint32_t cnt[E], ties = 0, omax = 0;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const uint32_t mm = sb[e] >> 9;
+            const uint32_t mm = (sb[e] >> 9) & 63u;
             cnt[e] = mm ? 1u << 16 : 0u;
             omax = max(omax, mm ? mm - 1u : 0u);
         }
@@ -1406,13 +1422,13 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
             uint32_t pq[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                const uint32_t b0 = sb[e] & 511u, mm = sb[e] >> 9;
-                const uint32_t self = (uint32_t)(e * 64 + lane) - b0;
+                const uint32_t b0 = sb[e] & 511u, mm = (sb[e] >> 9) & 63u;
+                const uint32_t self = sb[e] >> 20;
                 pq[e] = L.idx[q + 1u < mm ? b0 + q + (q >= self ? 1u : 0u) : b0] >> 17;
             }
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                const bool in = q + 1u < (sb[e] >> 9);
+                const bool in = q + 1u < ((sb[e] >> 9) & 63u);
                 const uint32_t pk = iw[e] >> 17;
                 cnt[e] += (in & (pq[e] < pk) ? 1u : 0u) + (in & (pq[e] <= pk) ? 1u << 16 : 0u);
                 ties |= (in & (pq[e] == pk) ? 1u : 0u) << e;
@@ -1420,8 +1436,8 @@ __device__ __forceinline__ void wave_sort_bucket2_e(const uint8_t* __restrict__ 
         }
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const uint32_t p = (uint32_t)(e * 64 + lane);
-            const uint32_t b0 = sb[e] & 511u, mm = sb[e] >> 9;
+            const uint32_t b0 = sb[e] & 511u, mm = (sb[e] >> 9) & 63u;
+            const uint32_t p = b0 + (sb[e] >> 20);  // the element's position
             const bool mine = mm != 0;
             const uint32_t i = iw[e] & 0x1ffffu;
             uint32_t lt = cnt[e] & 0xffffu, le = cnt[e] >> 16, eqlt = 0;
