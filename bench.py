@@ -59,7 +59,7 @@ def ensure_built():
 # traffic (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic.py), issue (SQ/GRBM
 # counters, tools/issue.py) and kernel stats; each file records the sha256 of
 # the library it was measured with, and a file from another build is not used
-PROFILE_ROUND = "r05"
+PROFILE_ROUND = "r06"
 TRAFFIC_PROFILE = os.path.join(REPO, "profiles", PROFILE_ROUND + "_traffic_{name}.json")
 ISSUE_PROFILE = os.path.join(REPO, "profiles", PROFILE_ROUND + "_issue_{name}.json")
 KSTATS_PROFILE = "profiles/" + PROFILE_ROUND + "_kernel_stats_{name}.csv"
