@@ -309,6 +309,90 @@ __device__ void ha_depths(WaveList& a, int len) {
     }
 }
 
+// Phase 2 without the serial level walk when no length limit applies: the
+// depth of every internal node by pointer jumping over the parent pointers
+// (P, Dd: two LDS arrays of >= len ints, free after ha_parents), the internal
+// nodes per depth I_d by ballots, and the leaves per depth L_d = 2 I_(d-1) -
+// I_d assigned from the top of the sorted array, as allocateNodeLengths
+// (kernel.cpp:2722-2739) assigns them level by level.  Returns false (and
+// leaves `a` untouched) when the deepest leaf would pass kMaxCodeLen, the
+// reference's relocation case (findNodesToRelocate's test, :2714-2720 /
+// :2807-2811), which ha_depths then runs.
+__device__ bool ha_depths_fast(WaveList& a, int len, int* P, int* Dd) {
+    const int lane = lane_id();
+    const int root = len - 2;
+    int dep[5];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+        const int k = r * 64 + lane;
+        const int v = r == 0 ? a.r0 : r == 1 ? a.r1 : r == 2 ? a.r2 : r == 3 ? a.r3 : a.r4;
+        dep[r] = k < root ? 1 : 0;
+        if (k < len) {
+            P[k] = k < root ? mod_len(v, len) : k;
+            Dd[k] = dep[r];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // jumps register by register: a node read later in a round may already
+    // have jumped, which only speeds it up -- each (P, Dd) pair is read
+    // between the two writes of another register's update, never across them
+    for (int round = 0; round < 12; ++round) {
+        bool moved = false;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const int k = r * 64 + lane;
+            if (k < len) {
+                const int p = P[k];
+                const int pp = P[p], dp = Dd[p];
+                moved |= pp != p;
+                dep[r] += dp;
+                Dd[k] = dep[r];
+                P[k] = pp;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!__ballot(moved)) break;
+    }
+    // deepest internal node (node 0 in a Huffman tree; the maximum for safety)
+    int dmax = 0;
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+        if (r * 64 + lane < len - 1) dmax = max(dmax, dep[r]);
+    dmax = (int)__builtin_amdgcn_readlane((int)wave_incl_max((uint32_t)dmax), 63);
+    if (dmax + 1 > kMaxCodeLen) return false;
+    // internal nodes per depth: lane d holds I_d
+    int icnt = 0;
+    for (int d = 1; d <= dmax; ++d) {
+        int id = 0;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) id += __popcll(__ballot(r * 64 + lane < len - 1 && dep[r] == d));
+        icnt = lane == d ? id : icnt;
+    }
+    // leaves: depth 1 + #{d : cum_d <= rank from the top}, cum_d = sum of
+    // L_e = 2 I_(e-1) - I_e over e <= d (I_0 = 1, the root)
+#pragma unroll
+    for (int r = 0; r < 5; ++r) dep[r] = 1;
+    int iprev = 1, cum = 0;
+    for (int d = 1; d <= dmax; ++d) {
+        const int id = __builtin_amdgcn_readlane(icnt, d);
+        cum += 2 * iprev - id;
+        iprev = id;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) dep[r] += (len - 1 - (r * 64 + lane)) >= cum ? 1 : 0;
+    }
+    a.r0 = lane < len ? dep[0] : a.r0;
+    a.r1 = lane + 64 < len ? dep[1] : a.r1;
+    a.r2 = lane + 128 < len ? dep[2] : a.r2;
+    a.r3 = lane + 192 < len ? dep[3] : a.r3;
+    a.r4 = lane + 256 < len ? dep[4] : a.r4;
+    return true;
+}
+
+// BZ2MI_HUF_FASTDEPTHS (default): ha_depths_fast before the serial walk
+#ifndef BZ2MI_HUF_FASTDEPTHS
+#define BZ2MI_HUF_FASTDEPTHS 1
+#endif
+constexpr bool kHufFastDepths = BZ2MI_HUF_FASTDEPTHS != 0;
 __device__ __forceinline__ int table_count(int m) {
     return m >= 2400 ? 6 : m >= 1200 ? 5 : m >= 600 ? 4 : m >= 200 ? 3 : 2;
 }
@@ -375,7 +459,8 @@ __device__ void build_table(HufShared& sh, int q, int alpha, bool stamp = false)
         ha_parents(A, tf, alpha);  // (tf[q] is free: keys are in registers)
         BZ2MI_PHASE(g_huf_phase, 14, stamp);
         a.load(A, alpha);
-        ha_depths(a, alpha);
+        // (A and tf are free again: the pointers are in registers)
+        if (!kHufFastDepths || !ha_depths_fast(a, alpha, A, tf)) ha_depths(a, alpha);
         BZ2MI_PHASE(g_huf_phase, 15, stamp);
     } else {
         a.load(A, alpha);

@@ -177,3 +177,39 @@ def test_unit_assemble_waits_for_null_stream_users():
     assert nbytes == m
     assert torch.equal(buf[:m], ref[:m])
     u.close()
+
+
+@pytest.mark.timeout(600)
+def test_c4_mixed_512mib_matches_cpuref(cpuref):
+    """Config C4's data against the C restatement, not only against the
+    device's own single call: the first 512 MiB of the C4 stream (eight 64 MiB
+    segments of random, text, run-heavy and ACGT bytes) compressed by
+    compress_device at -9, p = 10 and, cut into 4 stream units (the layout
+    the 8-GPU configuration shards), by the unit protocol -- both equal to
+    cpu_ref's stream (pinned to O_ref) byte for byte."""
+    n = 512 << 20
+    host = c4_stream(n)
+    want = cpuref.compress(host.tobytes(), 9, 10, threads=_threads())
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy(host).to(dev)
+    cap = bz2mi.compress_bound(n, 9, 10000)
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ctx = bz2mi.Context(9, 10, 10000)
+    m = ctx.compress_device(x.data_ptr(), n, out.data_ptr(), cap)
+    assert out[:m].cpu().numpy().tobytes() == want
+    K, halo = 4, bz2mi.unit_halo(9, 10000)
+    U = n // K
+    units = {}
+    for g in range(K):
+        a, b = g * U, (g + 1) * U
+        end = min(n, b + halo)
+        u = shard.DeviceUnit(ctx, dev)
+        u.begin(x[a:end].clone(), b - a, end - b, end == n)
+        units[g] = u
+    lay = shard.compress_units(units, [0] * K, 10, 9)
+    o2 = torch.zeros(lay.stream_bytes + 64, dtype=torch.uint8, device=dev)
+    got = shard.gather_stream_device(lay, shard.settle(lay), o2, 9)
+    assert got.cpu().numpy().tobytes() == want
+    for u in units.values():
+        u.close()
+    ctx.close()
