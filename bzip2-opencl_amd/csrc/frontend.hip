@@ -460,18 +460,39 @@ __global__ __launch_bounds__(256) void fe_dmap_kernel(const uint8_t* __restrict_
     const uint64_t span = at <= lim_i ? lim_i - at : 0;
     const uint32_t lim_q = at <= lim_i ? (uint32_t)(span < 63u ? span : 63u) + 1u : 0u;  // bytes q < lim_q have entries
     const uint32_t sink = (uint32_t)kDmapMax + (uint32_t)lane;
+    // the byte before the lane's first (previous lane, previous chunk)
+    uint32_t vprev = (uint32_t)__shfl_up((int)(xv[15] >> 24), 1);
+    if (lane == 0) vprev = at > 0 ? (uint32_t)x[at - 1] : 0x100u;
 #pragma unroll
     for (int q = 0; q < 64; ++q) {
         const uint32_t ci = (kv[q >> 2] >> ((q & 3) * 8)) & 255u;
         const uint32_t vq = (xv[q >> 2] >> ((q & 3) * 8)) & 255u;
         const uint32_t vn = (xv[(q + 1) >> 2] >> (((q + 1) & 3) * 8)) & 255u;
         const uint32_t kn = (kv[(q + 1) >> 2] >> (((q + 1) & 3) * 8)) & 255u;
-        const uint32_t hi = (vn != vq) ? 16u : 0u;
+        uint32_t hi = (vn != vq) ? 16u : 0u;
+        // A block that would start at i+1 inside a run of 2 or 3 bytes that
+        // begins at i (x[i-1] != x[i] == x[i+1]) is written here as a fast
+        // step: the block's own run is the L-1 bytes [i+1, e), whose RLE1
+        // output is L-1 bytes, while the unsplit costs flush all L of them at
+        // e -- so its target is Fg(i+2) + 1 + S-6 (D one larger), what the
+        // chain's mid-run path (slow_from) computes with e and Fg(e+1).
+        // Longer runs (4+: count bytes, pieces) keep that path.
+        uint32_t dadj = 0;
+        if (hi == 0u && q + 3 <= 66) {
+            const uint32_t v2 = (xv[(q + 2) >> 2] >> (((q + 2) & 3) * 8)) & 255u;
+            const uint32_t v3 = (xv[(q + 3) >> 2] >> (((q + 3) & 3) * 8)) & 255u;
+            const uint32_t vp = q == 0 ? vprev : (xv[(q - 1) >> 2] >> (((q - 1) & 3) * 8)) & 255u;
+            const bool short_run = vp != vq && (v2 != vn || v3 != v2) && at + (uint64_t)q + 3 < n;
+            if (short_run) {
+                hi = 16u;
+                dadj = 1u;
+            }
+        }
         const bool has = ci != 0 && (uint32_t)q < lim_q;
-        st[has ? fl : sink] = (uint8_t)(((ci + kn) & 15u) | hi);
+        st[has ? fl : sink] = (uint8_t)(((ci + kn + dadj) & 15u) | hi);
         if (has && ci > 1) {
 #pragma unroll
-            for (uint32_t r = 1; r < 5; ++r) st[r < ci ? fl + r : sink] = (uint8_t)(((ci + kn - r) & 15u) | hi);
+            for (uint32_t r = 1; r < 5; ++r) st[r < ci ? fl + r : sink] = (uint8_t)(((ci + kn + dadj - r) & 15u) | hi);
         }
         fl += ci;
     }
