@@ -395,7 +395,7 @@ int run_window(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint64_t start, boo
         for (size_t i = 0; i < nc; ++i) rows[i] = row[chain[i]];
         DCHECK(hipMemcpyAsync(d->d_blocks, chain.data(), nc * sizeof(uint32_t), hipMemcpyHostToDevice, s));
         DCHECK(hipMemcpyAsync(d->d_blocks + nc, rows.data(), nc * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(dec_mtf_kernel, dim3((unsigned)nc), dim3(64), 0, s, d->d_syms, sym_stride, d->d_symmap,
+        hipLaunchKernelGGL(dec_mtf_kernel, dim3((unsigned)nc), dim3(kDecMtfThreads), 0, s, d->d_syms, sym_stride, d->d_symmap,
                            d->d_blocks, d->d_blocks + nc, (uint32_t)nc, smax, d->d_merged, sym_stride, d->d_bwt,
                            stride, d->d_info);
         DCHECK(hipGetLastError());

@@ -512,11 +512,42 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
 //           consecutive symbols, offsets by a wave scan of the byte counts).
 // A symbol costs its lane ~rank/4 LDS word shifts instead of a serial pass
 // of the whole wave.
+// BZ2MI_MTF_QUAD (default): the recency list as 16-byte quads ([quad][lane],
+// entry 16q + 4j + i in byte i of word j), so a move to front shifts 16
+// entries per LDS read/write pair instead of 4.
+#ifndef BZ2MI_MTF_QUAD
+#define BZ2MI_MTF_QUAD 1
+#endif
+#ifndef BZ2MI_MTF_QGROUP
+#define BZ2MI_MTF_QGROUP 4
+#endif
+#ifndef BZ2MI_MTF_PREFETCH
+#define BZ2MI_MTF_PREFETCH 16
+#endif
+// BZ2MI_MTF_WAVES (decode.hpp): waves per block in pass A (chunks = 64 x
+// waves); passes B + C run on wave 0.
+constexpr uint32_t kMW = BZ2MI_MTF_WAVES;
+constexpr uint32_t kMC = 64 * kMW;  // chunks per block
 struct MtfLds {
-    uint32_t rec[64][64];    // [word][lane] recency list, entry 4w+j in byte j
-    uint32_t used[8][64];    // [word][lane] start indices taken
+#if BZ2MI_MTF_QUAD
+    uint4 rec4[16][kMC];     // [quad][chunk] recency list
+#else
+    uint32_t rec[64][kMC];   // [word][chunk] recency list, entry 4w+j in byte j
+#endif
+    uint32_t used[8][kMC];   // [word][chunk] start indices taken
+    uint32_t ca[kMC];        // chunk starts
+    uint32_t cnt[kMC];       // chunk byte counts -> output offsets
     uint8_t lists[2][256];   // start lists of chunk c and c+1, as output bytes
 };
+
+// word w (entries 4w..4w+3) of lane `lane`'s recency list
+__device__ __forceinline__ uint32_t& rec_word(MtfLds& L, uint32_t w, uint32_t lane) {
+#if BZ2MI_MTF_QUAD
+    return reinterpret_cast<uint32_t*>(&L.rec4[w >> 2][lane])[w & 3];
+#else
+    return L.rec[w][lane];
+#endif
+}
 
 __device__ __forceinline__ uint32_t select_zero(uint32_t u, uint32_t k) {
     // index of the k-th (0-based) zero bit of u, LSB first (k < popc(~u))
@@ -533,7 +564,7 @@ __device__ __forceinline__ uint32_t select_zero(uint32_t u, uint32_t k) {
     return pos;
 }
 
-__global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict__ syms, size_t sym_stride,
+__global__ __launch_bounds__(kDecMtfThreads) void dec_mtf_kernel(const uint16_t* __restrict__ syms, size_t sym_stride,
                                                      const uint8_t* __restrict__ symmaps,
                                                      const uint32_t* __restrict__ blocks,
                                                      const uint32_t* __restrict__ sym_row, uint32_t nblocks,
@@ -544,25 +575,27 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
     const uint32_t bi = blockIdx.x;
     if (bi >= nblocks) return;
     const int lane = lane_id();
+    const uint32_t ch = threadIdx.x;  // this thread's chunk
     const uint32_t k = uniform(blocks[bi]);
     DecBlockInfo* info = infos + k;
     const uint32_t ns = uniform(info->nsym), eob = uniform(info->alpha) + 1, orig = uniform(info->orig);
     const uint16_t* so = syms + (size_t)sym_row[bi] * sym_stride;
     uint32_t* tv = scratch + (size_t)bi * sstride;
     uint8_t* out = bwt + (size_t)bi * stride;  // (rows by chain position)
-    // chunk [a, b): nominal 64th, start moved past run digits
-    uint32_t a = (uint32_t)((uint64_t)ns * (uint32_t)lane / 64u);
-    if (lane)
+    // chunk [a, b): nominal kMC-th, start moved past run digits
+    uint32_t a = (uint32_t)((uint64_t)ns * ch / kMC);
+    if (ch)
         while (a < ns && so[a] <= 1) ++a;
-    const uint32_t an = (uint32_t)__shfl_down((int)a, 1);
-    const uint32_t b = lane == 63 ? ns : an;
+    L.ca[ch] = a;
+    __syncthreads();
+    const uint32_t b = ch == kMC - 1 ? ns : L.ca[ch + 1];
     // ---- pass A
 #pragma unroll
-    for (int w = 0; w < 8; ++w) L.used[w][lane] = 0;
+    for (int w = 0; w < 8; ++w) L.used[w][ch] = 0;
     uint32_t D = 0, run = 0, inc = 1, runpos = 0, cnt = 0;
     bool inrun = false;
     auto flush_run = [&]() {
-        const uint32_t front = D ? (L.rec[0][lane] & 255u) : 0u;
+        const uint32_t front = D ? (rec_word(L, 0, ch) & 255u) : 0u;
         tv[runpos] = front | (run << 8);
         cnt += run;
         inrun = false;
@@ -608,13 +641,13 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
         const uint32_t r = s - 1;
         uint32_t v, rr;
         if (r < D) {
-            v = (L.rec[r >> 2][lane] >> (8 * (r & 3))) & 255u;
+            v = (rec_word(L, r >> 2, ch) >> (8 * (r & 3))) & 255u;
             rr = r;
         } else {
             uint32_t kk = r - D;
             v = 255u;
             for (int w = 0; w < 8; ++w) {
-                const uint32_t u = L.used[w][lane];
+                const uint32_t u = L.used[w][ch];
                 const uint32_t z = 32u - (uint32_t)__popc(u);
                 if (kk < z) {
                     v = (uint32_t)w * 32u + select_zero(u, kk);
@@ -622,7 +655,7 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
                 }
                 kk -= z;
             }
-            L.used[v >> 5][lane] |= 1u << (v & 31);
+            L.used[v >> 5][ch] |= 1u << (v & 31);
             rr = D;
             D++;
         }
@@ -631,19 +664,51 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
         uint32_t carry = v;
         const uint32_t wl = rr >> 2;
         const uint32_t mlast = (rr & 3) == 3 ? 0xffffffffu : ((1u << (8 * ((rr & 3) + 1))) - 1u);
+#if BZ2MI_MTF_QUAD
+        // quads in groups of kQG: reads in flight, then the shifts
+        constexpr uint32_t kQG = BZ2MI_MTF_QGROUP;
+        const uint32_t ql = rr >> 4, cj = wl & 3u;
+        for (uint32_t g0 = 0; g0 <= ql; g0 += kQG) {
+            uint4 o[kQG];
+#pragma unroll
+            for (uint32_t i = 0; i < kQG; ++i) o[i] = g0 + i <= ql ? L.rec4[g0 + i][ch] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t i = 0; i < kQG; ++i) {
+                const uint32_t q = g0 + i;
+                if (q > ql) break;
+                uint4 sh;
+                sh.x = (o[i].x << 8) | carry;
+                sh.y = __builtin_amdgcn_alignbit(o[i].y, o[i].x, 24);
+                sh.z = __builtin_amdgcn_alignbit(o[i].z, o[i].y, 24);
+                sh.w = __builtin_amdgcn_alignbit(o[i].w, o[i].z, 24);
+                carry = o[i].w >> 24;
+                if (q < ql) {
+                    L.rec4[q][ch] = sh;
+                } else {
+                    const uint32_t m0 = cj > 0 ? 0xffffffffu : mlast;
+                    const uint32_t m1 = cj > 1 ? 0xffffffffu : cj == 1 ? mlast : 0u;
+                    const uint32_t m2 = cj > 2 ? 0xffffffffu : cj == 2 ? mlast : 0u;
+                    const uint32_t m3 = cj == 3 ? mlast : 0u;
+                    L.rec4[q][ch] = make_uint4((sh.x & m0) | (o[i].x & ~m0), (sh.y & m1) | (o[i].y & ~m1),
+                                                 (sh.z & m2) | (o[i].z & ~m2), (sh.w & m3) | (o[i].w & ~m3));
+                }
+            }
+        }
+#else
         for (uint32_t g0 = 0; g0 <= wl; g0 += 8) {
             uint32_t o[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) o[i] = g0 + i <= wl ? L.rec[g0 + i][lane] : 0u;
+            for (int i = 0; i < 8; ++i) o[i] = g0 + i <= wl ? L.rec[g0 + i][ch] : 0u;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const uint32_t w = g0 + i;
                 if (w > wl) break;
                 const uint32_t sh = (o[i] << 8) | carry;
                 carry = o[i] >> 24;
-                L.rec[w][lane] = w < wl ? sh : ((sh & mlast) | (o[i] & ~mlast));
+                L.rec[w][ch] = w < wl ? sh : ((sh & mlast) | (o[i] & ~mlast));
             }
         }
+#endif
         tv[p] = v | (1u << 8);
         cnt += 1;
     }
@@ -652,12 +717,12 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
     {
         uint32_t pos = D;
         for (int w = 0; w < 8 && pos < 256; ++w) {
-            uint32_t z = ~L.used[w][lane];
+            uint32_t z = ~L.used[w][ch];
             while (z && pos < 256) {
                 const uint32_t bit = (uint32_t)__builtin_ctz(z);
                 z &= z - 1;
                 const uint32_t e = (uint32_t)w * 32u + bit;
-                uint32_t& wd = L.rec[pos >> 2][lane];
+                uint32_t& wd = rec_word(L, pos >> 2, ch);
                 const uint32_t sh = 8 * (pos & 3);
                 wd = (wd & ~(0xffu << sh)) | (e << sh);
                 pos++;
@@ -668,19 +733,74 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
     // output bytes; list_0 = the symbol map), then the chunk's bytes -- lanes
     // take consecutive symbols, offsets by a wave scan of their byte counts --
     // then list_{c+1}[i] = list_c[perm_c[i]]
-    const uint32_t incl = wave_incl_sum(cnt);
-    const uint32_t total = uniform((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
-    const uint32_t cbase = incl - cnt;  // this lane's chunk offset
+    L.cnt[ch] = cnt;
+    __syncthreads();
+    if (ch >= 64) return;  // (passes B + C: wave 0)
+    uint32_t total;
+    {
+        // lane l: chunks l*kMW .. l*kMW+kMW-1 -> their output offsets
+        uint32_t cs[kMW], sum = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kMW; ++i) {
+            cs[i] = L.cnt[lane * kMW + i];
+            sum += cs[i];
+        }
+        const uint32_t incl = wave_incl_sum(sum);
+        total = uniform((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+        uint32_t acc = incl - sum;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t i = 0; i < kMW; ++i) {
+            L.cnt[lane * kMW + i] = acc;
+            acc += cs[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
     uint32_t status = total > smax ? (uint32_t)kDecSize : 0u;
     const uint8_t* smp = symmaps + (size_t)k * 256;
 #pragma unroll
     for (int j = 0; j < 4; ++j) L.lists[0][lane * 4 + j] = smp[lane * 4 + j];
     __builtin_amdgcn_wave_barrier();
-    for (int c = 0; c < 64 && !status; ++c) {
+    for (uint32_t c = 0; c < kMC && !status; ++c) {
         const uint8_t* lc = L.lists[c & 1];
-        const uint32_t ca = uniform((uint32_t)__builtin_amdgcn_readlane((int)a, c));
-        const uint32_t cb = uniform((uint32_t)__builtin_amdgcn_readlane((int)b, c));
-        uint32_t o = uniform((uint32_t)__builtin_amdgcn_readlane((int)cbase, c));
+        const uint32_t ca = uniform(L.ca[c]);
+        const uint32_t cb = c == kMC - 1 ? ns : uniform(L.ca[c + 1]);
+        uint32_t o = uniform(L.cnt[c]);
+#if BZ2MI_MTF_PREFETCH > 1
+        // the chunk's scratch words kPF 64-symbol steps at a time, the next
+        // kPF loaded while these are written out: one load in flight per
+        // step was a memory latency per 64 symbols (the wave walks the
+        // block's symbols serially here)
+        constexpr uint32_t kPF = BZ2MI_MTF_PREFETCH;
+        uint32_t xb[kPF];
+#pragma unroll
+        for (uint32_t i = 0; i < kPF; ++i) {
+            const uint32_t pn = ca + 64u * i + (uint32_t)lane;
+            xb[i] = pn < cb ? tv[pn] : 0u;
+        }
+        for (uint32_t p0 = ca; p0 < cb; p0 += 64u * kPF) {
+            uint32_t xc[kPF];
+#pragma unroll
+            for (uint32_t i = 0; i < kPF; ++i) {
+                xc[i] = xb[i];
+                const uint32_t pn = p0 + 64u * (kPF + i) + (uint32_t)lane;
+                xb[i] = pn < cb ? tv[pn] : 0u;
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kPF; ++i) {
+                if (p0 + 64u * i >= cb) break;
+                const uint32_t x = xc[i];
+                const uint32_t n1 = x >> 8;
+                const uint32_t inc1 = wave_incl_sum(n1);
+                uint32_t q = o + inc1 - n1;
+                if (n1) {
+                    const uint8_t byte = lc[x & 255u];
+                    for (uint32_t r2 = 0; r2 < n1; ++r2) out[q + r2] = byte;
+                }
+                o += (uint32_t)__builtin_amdgcn_readlane((int)inc1, 63);
+            }
+        }
+#else
         uint32_t xn = ca + (uint32_t)lane < cb ? tv[ca + lane] : 0u;  // one 64-symbol step ahead
         for (uint32_t p0 = ca; p0 < cb; p0 += 64) {
             const uint32_t x = xn;
@@ -695,11 +815,12 @@ __global__ __launch_bounds__(64) void dec_mtf_kernel(const uint16_t* __restrict_
             }
             o += (uint32_t)__builtin_amdgcn_readlane((int)inc1, 63);
         }
-        if (c < 63) {
+#endif
+        if (c < kMC - 1) {
             uint32_t nv[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t pi = (L.rec[lane][c] >> (8 * j)) & 255u;  // entry 4*lane + j of chunk c
+                const uint32_t pi = (rec_word(L, lane, c) >> (8 * j)) & 255u;  // entry 4*lane + j of chunk c
                 nv[j] = lc[pi];
             }
             __builtin_amdgcn_wave_barrier();
@@ -739,7 +860,7 @@ static_assert(kWalkers <= 0xffff, "walker ids fit 16 bits");
 #ifndef BZ2MI_IBWT_ONEWALK
 #define BZ2MI_IBWT_ONEWALK 1
 #endif
-constexpr uint32_t kWCap = 128;
+constexpr uint32_t kWCap = BZ2MI_IBWT_WCAP;
 static_assert((size_t)kWalkers * kWCap == kDecIbwtScratch, "walker scratch layout");
 
 struct IbwtLds {

@@ -55,7 +55,17 @@ __global__ void dec_huff_kernel(const uint8_t* in, uint64_t n, const DecCand* ca
 #endif
 constexpr int kDecSymBlocks = BZ2MI_SYM_BLOCKS;  // blocks per wave of dec_sym_kernel
 constexpr int kDecIbwtThreads = 1024;             // threads per dec_ibwt_kernel workgroup
-constexpr size_t kDecIbwtScratch = (size_t)kDecIbwtThreads * 8 * 128;  // walker bytes per dec_ibwt_kernel workgroup
+// waves per dec_mtf_kernel workgroup (pass A's chunks = 64 x waves): a 900 KB
+// batch has ~1,200 blocks, one wave each leaves most SIMDs one latency-bound wave
+#ifndef BZ2MI_MTF_WAVES
+#define BZ2MI_MTF_WAVES 1
+#endif
+constexpr uint32_t kDecMtfThreads = 64 * BZ2MI_MTF_WAVES;
+// bytes an inverse-BWT walker keeps of its segment (beyond: walked again)
+#ifndef BZ2MI_IBWT_WCAP
+#define BZ2MI_IBWT_WCAP 128
+#endif
+constexpr size_t kDecIbwtScratch = (size_t)kDecIbwtThreads * 8 * BZ2MI_IBWT_WCAP;  // walker bytes per dec_ibwt_kernel workgroup
 // symbol row j <- candidate sel[j]
 __global__ void dec_sym_kernel(const uint8_t* in, uint64_t n, const uint8_t* tabs, const uint32_t* sel, uint32_t nids,
                                uint32_t smax, uint16_t* syms, size_t sym_stride, DecBlockInfo* infos);
