@@ -524,9 +524,9 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
 #ifndef BZ2MI_MTF_PREFETCH
 #define BZ2MI_MTF_PREFETCH 16
 #endif
-// BZ2MI_MTF_WAVES (decode.hpp): waves per block in pass A (chunks = 64 x
+// BZ2MI_DMTF_WAVES (decode.hpp): waves per block in pass A (chunks = 64 x
 // waves); passes B + C run on wave 0.
-constexpr uint32_t kMW = BZ2MI_MTF_WAVES;
+constexpr uint32_t kMW = BZ2MI_DMTF_WAVES;
 constexpr uint32_t kMC = 64 * kMW;  // chunks per block
 struct MtfLds {
 #if BZ2MI_MTF_QUAD

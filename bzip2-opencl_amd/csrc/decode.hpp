@@ -57,10 +57,10 @@ constexpr int kDecSymBlocks = BZ2MI_SYM_BLOCKS;  // blocks per wave of dec_sym_k
 constexpr int kDecIbwtThreads = 1024;             // threads per dec_ibwt_kernel workgroup
 // waves per dec_mtf_kernel workgroup (pass A's chunks = 64 x waves): a 900 KB
 // batch has ~1,200 blocks, one wave each leaves most SIMDs one latency-bound wave
-#ifndef BZ2MI_MTF_WAVES
-#define BZ2MI_MTF_WAVES 1
+#ifndef BZ2MI_DMTF_WAVES
+#define BZ2MI_DMTF_WAVES 1
 #endif
-constexpr uint32_t kDecMtfThreads = 64 * BZ2MI_MTF_WAVES;
+constexpr uint32_t kDecMtfThreads = 64 * BZ2MI_DMTF_WAVES;
 // bytes an inverse-BWT walker keeps of its segment (beyond: walked again)
 #ifndef BZ2MI_IBWT_WCAP
 #define BZ2MI_IBWT_WCAP 128

@@ -46,25 +46,6 @@ __device__ __forceinline__ uint32_t piece_cost(uint32_t len) {  // output bytes 
     return len >= 4 ? 5u : len;
 }
 
-// 64 bytes of lane `l` of the chunk at c0 (zero beyond n)
-__device__ __forceinline__ void load64(const uint8_t* x, uint64_t n, uint64_t at, uint8_t* v) {
-    if (at + 64 <= n) {
-        const uint4* p = (const uint4*)(x + at);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint4 w = p[q];
-            uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int s = 0; s < 4; ++s) v[q * 16 + r * 4 + s] = (uint8_t)(ww[r] >> (8 * s));
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < 64; ++q) v[q] = (at + q < n) ? x[at + q] : 0;
-    }
-}
-
 // the 64 bytes of lane `l` of a chunk as 16 dwords (zero beyond n)
 __device__ __forceinline__ void load16w(const uint8_t* x, uint64_t n, uint64_t at, uint32_t (&w)[16]) {
     if (at + 64 <= n) {
@@ -84,8 +65,6 @@ __device__ __forceinline__ void load16w(const uint8_t* x, uint64_t n, uint64_t a
         }
     }
 }
-
-__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[16], int q) { return (w[q >> 2] >> (8 * (q & 3))) & 255u; }
 
 // bit q: byte q of the lane's 64 differs from the byte before it (byte 0:
 // from `prev_last`), by SWAR on the dwords
