@@ -257,9 +257,14 @@ int run_window(bz2mi_dctx* d, const uint8_t* d_in, size_t n, uint64_t start, boo
         if (!sel.empty()) {
             if ((r = grow(&d->d_syms, &d->syms_cap, sel.size() * sym_stride))) return r;
             DCHECK(hipMemcpyAsync(d->d_ids + nk, sel.data(), sel.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+#if BZ2MI_SYM_WINDOW
+            hipLaunchKernelGGL(dec_symw_kernel, dim3((unsigned)sel.size()), dim3(64), 0, s, d_in, (uint64_t)n,
+                               d->d_tabs, d->d_ids + nk, (uint32_t)sel.size(), smax, d->d_syms, sym_stride, d->d_info);
+#else
             hipLaunchKernelGGL(dec_sym_kernel, dim3((unsigned)((sel.size() + kDecSymBlocks - 1) / kDecSymBlocks)),
                                dim3(64), 0, s, d_in, (uint64_t)n, d->d_tabs, d->d_ids + nk, (uint32_t)sel.size(), smax,
                                d->d_syms, sym_stride, d->d_info);
+#endif
             DCHECK(hipGetLastError());
             DCHECK(hipMemcpyAsync(info.data(), d->d_info, nk * sizeof(DecBlockInfo), hipMemcpyDeviceToHost, s));
         }

@@ -495,6 +495,207 @@ __global__ __launch_bounds__(64) void dec_sym_kernel(const uint8_t* __restrict__
     info->end_bit = br.pos;
 }
 
+// ---- K2s, windowed (BZ2MI_SYM_WINDOW, the default): one block per wave.
+// The wave's 64 lanes look up the codes that would start at bit offsets
+// 0..63 of the reader's 128-bit window at once (one LDS gather), and the
+// block's serial chain then hops through those lookups -- offset o, its
+// entry (a lane read), o += the code length -- on the scalar unit, a few
+// instructions per symbol instead of a dependent LDS lookup and shift each.
+// A window ends past offset 63, at a group boundary (the next group's table)
+// or at a code longer than the lookup (the reference's limit / base walk on
+// the window's bits).  Symbols collect one per lane and leave 64 at a time.
+__global__ __launch_bounds__(64) void dec_symw_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                      const uint8_t* __restrict__ tabs, const uint32_t* __restrict__ sel,
+                                                      uint32_t nids, uint32_t smax, uint16_t* __restrict__ syms,
+                                                      size_t sym_stride, DecBlockInfo* __restrict__ infos) {
+    static_assert(kTabLimit == kMaxTables * (1 << kLutBits) * 2, "table layout");
+    static_assert(kTabSel % 4 == 0 && kTabBytes - kTabSel >= (kDecMaxSel / 4 + 2) * 4, "selector words");
+    __shared__ uint32_t lut32[kTabLimit / 4];
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t k = blockIdx.x;
+    if (k >= nids) return;
+    const uint32_t id = uniform(sel[k]);
+    DecBlockInfo* info = infos + id;
+    if (uniform(info->status)) return;
+    const uint8_t* tb = tabs + (size_t)id * kTabBytes;
+    {
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(tb);
+        for (uint32_t i = lane; i < (uint32_t)(kTabLimit / 4); i += 64) lut32[i] = s32[i];
+    }
+    __syncthreads();
+    const uint16_t* lut = reinterpret_cast<const uint16_t*>(lut32);
+    const int32_t* lim = reinterpret_cast<const int32_t*>(tb + kTabLimit);
+    const int32_t* bas = reinterpret_cast<const int32_t*>(tb + kTabBase);
+    const uint16_t* per = reinterpret_cast<const uint16_t*>(tb + kTabPerm);
+    const uint8_t* sg = tb + kTabSel;
+    const uint32_t nsel = uniform(info->nsel), eob = uniform(info->alpha) + 1;
+    // the reader: the stream's words wb..wb+127 one per lane in two vector
+    // registers (ra: the current 64, byte-swapped; rb: the next 64 as loaded,
+    // a ring ahead -- vector loads, untouched until the window reaches them,
+    // so no wait on them stalls the chain), the position `bo` bits into ra.
+    // Indices are clamped to the last whole word and the words from there
+    // on fixed up when a window reaches them.
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(in);  // (4-byte aligned)
+    const uint64_t nfull = n >> 2;
+    uint32_t tailw = 0;  // the last partial word, zero-padded
+    for (uint32_t q = 0; q < (uint32_t)(n & 3u); ++q) tailw |= (uint32_t)in[nfull * 4 + q] << (24 - 8 * q);
+    // (a block candidate needs more than 4 bytes: nfull >= 1)
+    auto raw_word = [&](uint64_t w0) -> uint32_t { return w32[min(w0 + lane, nfull - 1)]; };
+    const uint64_t p0 = uniform64(info->data_bit);
+    uint64_t wb = p0 >> 5;
+    uint32_t bo = (uint32_t)(p0 & 31u);
+    uint32_t ra = raw_word(wb), rb = raw_word(wb + 64);
+    uint16_t* so = syms + (size_t)k * sym_stride;
+    const uint32_t ns_max = smax + 2;
+    uint32_t g = 0, gleft = kGroupRun, ns = 0, status = 0;
+    // selectors four to a word, the next word loaded ahead (the words past
+    // nsel are inside the table area: kTabBytes holds the maximum + padding)
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sg);
+    uint32_t swc = sw[0], swn = sw[1];
+    uint32_t tsel = swc & 255u;
+    bool done = false;
+    // one ring of 64 words: windows while the position is in `cur`; then the
+    // ring after `nxt` is loaded into `cur`'s register (the two swap roles,
+    // so a load is only waited for a whole ring later)
+    auto run_ring = [&](uint32_t& cur, const uint32_t& nxt) {
+      const uint32_t cs = __builtin_bswap32(cur);
+      while (!done && bo < 64 * 32) {
+        // words wi..wi+4 (the window: 128 bits from bit `off` of word wi)
+        const uint32_t wi = bo >> 5, off = bo & 31u;
+        uint32_t a[5];
+        if (wi + 4 < 64) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) a[q] = (uint32_t)__builtin_amdgcn_readlane((int)cs, (int)(wi + q));
+        } else {
+            const uint32_t ns2 = __builtin_bswap32(nxt);
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const uint32_t j = wi + q;
+                const uint32_t xa = (uint32_t)__builtin_amdgcn_readlane((int)cs, (int)(j & 63u));
+                const uint32_t xb = (uint32_t)__builtin_amdgcn_readlane((int)ns2, (int)(j & 63u));
+                a[q] = j < 64 ? xa : xb;
+            }
+        }
+        if (wb + wi + 4 >= nfull) {  // the stream's end: its partial word, zeros after
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const uint64_t j = wb + wi + q;
+                a[q] = j < nfull ? a[q] : j == nfull ? tailw : 0u;
+            }
+        }
+        const uint64_t x0 = ((uint64_t)a[0] << 32) | a[1], x1 = ((uint64_t)a[2] << 32) | a[3];
+        const uint64_t x2 = (uint64_t)a[4] << 32;
+        const uint64_t whi = off ? (x0 << off) | (x1 >> (64 - off)) : x0;
+        const uint64_t wlo = off ? (x1 << off) | (x2 >> (64 - off)) : x1;
+        const uint64_t vj = lane ? (whi << lane) | (wlo >> (64 - lane)) : whi;
+        const uint32_t ev = lut[(tsel << kLutBits) + (uint32_t)(vj >> (64 - kLutBits))];
+        // chain words: the entry, or 0 (length 0) where the chain must stop
+        // for the per-symbol path -- a code longer than the lookup, or the
+        // end-of-block symbol
+        const uint32_t cw = (ev == kLong || (ev & 0xfffu) == eob) ? 0u : ev;
+        // the fast hops: up to `budget` ordinary symbols (the group's rest,
+        // the size limit), visited offsets marked in `vis`
+        const uint32_t budget = min(gleft, ns_max - ns);
+        uint64_t vis = 0;
+        uint32_t o = 0, cnt = 0;
+        bool special = false;
+        for (;;) {
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cw, (int)o);
+            const uint32_t len = c >> 12;
+            if (len == 0) {
+                special = true;
+                break;
+            }
+            vis |= 1ull << o;
+            o += len;
+            if (++cnt == budget || o >= 64) break;
+        }
+        // the window's symbols: the visited lanes in order (offsets increase)
+        if ((vis >> lane) & 1u) {
+            const uint32_t rk = (uint32_t)__popcll(vis & ((1ull << lane) - 1ull));
+            so[ns + rk] = (uint16_t)(ev & 0xfffu);
+        }
+        ns += cnt;
+        gleft -= cnt;
+        if (!special) {
+            if (ns >= ns_max) {  // (an ordinary symbol: not the end of block)
+                status = kDecSize;
+                done = true;
+            }
+        } else {
+            // one symbol the slow way: a long code (the reference's limit /
+            // base walk on the window's bits) or the end of block
+            const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)ev, (int)o);
+            uint32_t sym = e & 0xfffu, len = e >> 12;
+            if (e == kLong) {
+                const uint64_t x = o ? (whi << o) | (wlo >> (64 - o)) : whi;
+                const int32_t* lt = lim + tsel * (kMaxDecLen + 2);
+                const int32_t* bt = bas + tsel * (kMaxDecLen + 2);
+                sym = 0xffffffffu;
+                len = 0;
+                for (uint32_t l2 = kLutBits + 1; l2 <= (uint32_t)kMaxDecLen; ++l2) {
+                    const int32_t cv = (int32_t)(x >> (64 - l2));
+                    if (cv <= lt[l2]) {
+                        len = l2;
+                        sym = per[tsel * kMaxAlpha + (uint32_t)(cv + bt[l2])];
+                        break;
+                    }
+                }
+            }
+            if (sym == 0xffffffffu) {
+                status = kDecData;
+                done = true;
+            } else {
+                if (lane == 0) so[ns] = (uint16_t)sym;
+                ++ns;
+                o += len;
+                --gleft;
+                if (sym == eob || ns >= ns_max) {
+                    if (sym != eob) status = kDecSize;
+                    done = true;
+                }
+            }
+        }
+        if (!done && gleft == 0) {  // next group of 50 (HuffmanStageDecoder.hpp:50-57): its table
+            if (++g >= nsel) {
+                status = kDecData;
+                done = true;
+            } else {
+                if ((g & 3u) == 0) {
+                    swc = swn;
+                    swn = sw[(g >> 2) + 1];
+                }
+                tsel = (swc >> (8 * (g & 3u))) & 255u;
+                gleft = kGroupRun;
+            }
+        }
+        bo += o;
+      }
+      if (!done) {
+          bo -= 64 * 32;
+          wb += 64;
+          cur = raw_word(wb + 64);
+      }
+    };
+    while (!done) {
+        run_ring(ra, rb);
+        if (done) break;
+        run_ring(rb, ra);
+    }
+    // zeros up to the next multiple of 64 symbols (inside the stride)
+    {
+        const uint32_t z = (ns & ~63u) + lane;
+        if (z >= ns && (ns & 63u)) so[z] = 0;
+    }
+    const uint64_t pos = wb * 32 + bo;
+    if (pos > n * 8) status = kDecData;
+    if (lane == 0) {
+        info->status = status;
+        info->nsym = ns;
+        info->end_bit = pos;
+    }
+}
+
 // ---- K2b: data, part 2 (BlockDecompressor::decodeHuffmanData :177-231):
 // RUNA/RUNB runs and inverse move-to-front, one wave per block of the chain.
 // Lane c takes the c-th 64th of the block's symbols (its start moved past run

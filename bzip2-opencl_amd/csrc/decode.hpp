@@ -69,6 +69,12 @@ constexpr size_t kDecIbwtScratch = (size_t)kDecIbwtThreads * 8 * BZ2MI_IBWT_WCAP
 // symbol row j <- candidate sel[j]
 __global__ void dec_sym_kernel(const uint8_t* in, uint64_t n, const uint8_t* tabs, const uint32_t* sel, uint32_t nids,
                                uint32_t smax, uint16_t* syms, size_t sym_stride, DecBlockInfo* infos);
+__global__ void dec_symw_kernel(const uint8_t* in, uint64_t n, const uint8_t* tabs, const uint32_t* sel, uint32_t nids,
+                                uint32_t smax, uint16_t* syms, size_t sym_stride, DecBlockInfo* infos);
+// the windowed symbol decoder (one block per wave) instead of dec_sym_kernel
+#ifndef BZ2MI_SYM_WINDOW
+#define BZ2MI_SYM_WINDOW 1
+#endif
 // chain block i: candidate blocks[i], symbol row sym_row[i]; BWT row i
 __global__ void dec_mtf_kernel(const uint16_t* syms, size_t sym_stride, const uint8_t* symmaps,
                                const uint32_t* blocks, const uint32_t* sym_row, uint32_t nblocks, uint32_t smax,
