@@ -599,6 +599,31 @@ __global__ __launch_bounds__(64) void dec_symw_kernel(const uint8_t* __restrict_
         uint64_t vis = 0;
         uint32_t o = 0, cnt = 0;
         bool special = false;
+#if BZ2MI_SYM_PAIRS
+        // two hops at a time: lane j also holds the length of the code that
+        // follows its own (0: special or past the window)
+        uint32_t pw;
+        {
+            const uint32_t l1 = cw >> 12, j2 = lane + l1;
+            const uint32_t c2 = (uint32_t)__shfl((int)cw, (int)(j2 & 63u));
+            const uint32_t l2 = (l1 && j2 < 64) ? (c2 >> 12) : 0u;
+            pw = l1 | (l2 << 8);
+        }
+        for (;;) {
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pw, (int)o);
+            const uint32_t l1 = c & 0xffu, l2 = c >> 8;
+            if (l1 == 0) {
+                special = true;
+                break;
+            }
+            // (branch-free: t = 1 takes both)
+            const uint32_t t = (uint32_t)(l2 != 0) & (uint32_t)(cnt + 2 <= budget);
+            vis |= (1ull | ((uint64_t)t << l1)) << o;
+            o += l1 + (l2 & (0u - t));
+            cnt += 1 + t;
+            if (cnt == budget || o >= 64) break;
+        }
+#else
         for (;;) {
             const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cw, (int)o);
             const uint32_t len = c >> 12;
@@ -610,6 +635,7 @@ __global__ __launch_bounds__(64) void dec_symw_kernel(const uint8_t* __restrict_
             o += len;
             if (++cnt == budget || o >= 64) break;
         }
+#endif
         // the window's symbols: the visited lanes in order (offsets increase)
         if ((vis >> lane) & 1u) {
             const uint32_t rk = (uint32_t)__popcll(vis & ((1ull << lane) - 1ull));
@@ -1386,6 +1412,9 @@ __global__ __launch_bounds__(kIT) void dec_ibwt_kernel(const uint8_t* __restrict
 // the run byte k+1 more... the reference emits k+1 copies of the run byte,
 // the fourth included.  pass 0 counts (per chunk and entry state), pass 1
 // writes; chunk c of a block covers [c*n/256, (c+1)*n/256).
+#ifndef BZ2MI_RLE1_VEC16
+#define BZ2MI_RLE1_VEC16 1
+#endif
 namespace {
 struct Rle1Step {
     uint32_t st;
@@ -1501,6 +1530,47 @@ __global__ __launch_bounds__(256) void dec_rle1_kernel(const uint8_t* __restrict
     uint64_t o = base + off;
     uint32_t st = cs & 7u, prev = prev0;
     uint32_t r = 0;  // CRC register from 0
+#if BZ2MI_RLE1_VEC16
+    // the output collects in the 16-byte aligned block that holds o and
+    // leaves in one 16-byte store when the block is the chunk's own; the
+    // chunk's first and last blocks (shared with the neighbours) byte-wise.
+    // (A byte store per output byte was an L2 write request per byte.)
+    const uint64_t ostart = o;
+    const uint64_t ao = (uint64_t)(reinterpret_cast<uintptr_t>(out) & 15u);  // (blocks by address)
+    uint32_t b0w = 0, b1w = 0, b2w = 0, b3w = 0;
+    // bytes [lo, hi) of the block at index blk (out + blk 16-byte aligned;
+    // blk may lie before the output's start: then lo > 0 skips to ostart)
+    auto flush = [&](int64_t blk, uint32_t hi) {
+        const uint32_t lo = blk >= (int64_t)ostart ? 0u : (uint32_t)((int64_t)ostart - blk);
+        if (lo == 0 && hi == 16 && (uint64_t)blk + 16 <= cap) {
+            *reinterpret_cast<uint4*>(out + blk) = make_uint4(b0w, b1w, b2w, b3w);
+        } else {
+            const uint32_t wv[4] = {b0w, b1w, b2w, b3w};
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (j >= lo && j < hi && (uint64_t)(blk + j) < cap) out[blk + j] = (uint8_t)(wv[j >> 2] >> (8 * (j & 3)));
+        }
+        b0w = b1w = b2w = b3w = 0;
+    };
+    for_each_byte([&](uint32_t b) {
+        uint32_t e;
+        const uint32_t was = st;
+        st = rle1_next(st, b, prev, &e);
+        const uint32_t ob = was == 4 ? prev : b;  // a count byte repeats the run byte before it
+        for (uint32_t q = 0; q < e; ++q) {
+            const uint32_t pos = (uint32_t)((o + ao) & 15u), v = ob << (8 * (pos & 3u)), ws = pos >> 2;
+            b0w |= ws == 0 ? v : 0u;
+            b1w |= ws == 1 ? v : 0u;
+            b2w |= ws == 2 ? v : 0u;
+            b3w |= ws == 3 ? v : 0u;
+            o++;
+            if (pos == 15u) flush((int64_t)o - 16, 16u);
+            r = (r << 8) ^ ctab[(r >> 24) ^ ob];
+        }
+        prev = b;
+    });
+    if ((o + ao) & 15u) flush((int64_t)o - (int64_t)((o + ao) & 15u), (uint32_t)((o + ao) & 15u));
+#else
     for_each_byte([&](uint32_t b) {
         uint32_t e;
         const uint32_t was = st;
@@ -1513,6 +1583,7 @@ __global__ __launch_bounds__(256) void dec_rle1_kernel(const uint8_t* __restrict
         }
         prev = b;
     });
+#endif
     // block CRC: chunk registers shifted by the bytes after them
     const uint64_t after = total - (o - base);
     cpart[t] = crc_shift(r, after);
