@@ -599,7 +599,44 @@ __global__ __launch_bounds__(64) void dec_symw_kernel(const uint8_t* __restrict_
         uint64_t vis = 0;
         uint32_t o = 0, cnt = 0;
         bool special = false;
-#if BZ2MI_SYM_PAIRS
+#if BZ2MI_SYM_JUMP
+        // the chain by pointer jumping over the lanes: lane j's successor is
+        // j + its code length (64: past the window or a special lane, where
+        // the chain ends), R_j the offsets reachable from j; doubling until
+        // lane 0's jump leaves the window gives the whole chain from 0
+        {
+            const uint32_t l1 = cw >> 12;
+            const uint32_t nxu = lane + l1;
+            const bool spc = l1 == 0;
+            uint32_t J = spc ? 64u : min(nxu, 64u);
+            uint64_t R = 1ull << lane;
+            for (int k = 0; k < 6; ++k) {
+                if ((uint32_t)__builtin_amdgcn_readlane((int)J, 0) >= 64u) break;
+                const int src = (int)(J & 63u);
+                const uint32_t rlo = (uint32_t)__shfl((int)(uint32_t)R, src);
+                const uint32_t rhi = (uint32_t)__shfl((int)(uint32_t)(R >> 32), src);
+                const uint32_t jn = (uint32_t)__shfl((int)J, src);
+                const bool in = J < 64u;
+                R |= in ? (((uint64_t)rhi << 32) | rlo) : 0ull;
+                J = in ? jn : 64u;
+            }
+            const uint64_t orbit = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(R >> 32), 0) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)R, 0);
+            const uint64_t spm = __ballot(spc);
+            const uint64_t ord = orbit & ~spm;  // ordinary codes on the chain, in order
+            const uint32_t rk = (uint32_t)__popcll(ord & ((1ull << lane) - 1ull));
+            vis = __ballot(((ord >> lane) & 1u) && rk < budget);  // the first `budget` of them
+            cnt = (uint32_t)__popcll(vis);
+            if (cnt == budget) {  // stopped by the budget (even before a special code): after the last taken
+                o = (uint32_t)__builtin_amdgcn_readlane((int)nxu, 63 - __builtin_clzll(vis));
+            } else if (orbit & spm) {  // ended at a special code
+                o = (uint32_t)__builtin_ctzll(orbit & spm);
+                special = true;
+            } else {  // ran past the window
+                o = (uint32_t)__builtin_amdgcn_readlane((int)nxu, 63 - __builtin_clzll(ord));
+            }
+        }
+#elif BZ2MI_SYM_PAIRS
         // two hops at a time: lane j also holds the length of the code that
         // follows its own (0: special or past the window)
         uint32_t pw;

@@ -79,6 +79,10 @@ __global__ void dec_symw_kernel(const uint8_t* in, uint64_t n, const uint8_t* ta
 #ifndef BZ2MI_SYM_PAIRS
 #define BZ2MI_SYM_PAIRS 1
 #endif
+// ... or finds the window's whole chain by pointer jumping over the lanes
+#ifndef BZ2MI_SYM_JUMP
+#define BZ2MI_SYM_JUMP 1
+#endif
 // chain block i: candidate blocks[i], symbol row sym_row[i]; BWT row i
 __global__ void dec_mtf_kernel(const uint16_t* syms, size_t sym_stride, const uint8_t* symmaps,
                                const uint32_t* blocks, const uint32_t* sym_row, uint32_t nblocks, uint32_t smax,
