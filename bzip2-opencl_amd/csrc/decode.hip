@@ -145,6 +145,11 @@ struct BitReader {
     __device__ __forceinline__ uint32_t bit() { return bits(1); }
 };
 
+// BZ2MI_HUF_WORDPARSE (default): selectors and delta-coded lengths parsed a
+// word at a time (leading-ones count, pair flags) instead of bit by bit
+#ifndef BZ2MI_HUF_WORDPARSE
+#define BZ2MI_HUF_WORDPARSE 1
+#endif
 constexpr int kLutBits = 9;
 constexpr uint16_t kLong = 0xffff;
 constexpr int kMaxDecLen = 23;  // HUFFMAN_DECODE_MAXIMUM_CODE_LENGTH (Config.hpp:38)
@@ -167,23 +172,55 @@ __device__ __forceinline__ void fail(DecBlockInfo* info, uint32_t code) {
 
 // ---- K1: candidates.  Thread per 8-byte word of the stream: the 64 bit
 // positions starting in it, the 48-bit window read from 16 bytes.
+// BZ2MI_SCAN_HASH (default): a magic that starts in byte B of the thread's
+// word covers bytes B+1..B+4 completely, and those 32 bits are one of 16
+// values (2 magics x 8 bit offsets); a perfect hash of them ((w * K) >> 27,
+// 32 slots) tests each B with one LDS lookup, and only a hit runs the exact
+// test of its 8 bit positions (instead of 64 exact tests per thread).
+#ifndef BZ2MI_SCAN_HASH
+#define BZ2MI_SCAN_HASH 1
+#endif
+constexpr uint32_t kScanK = 0xcd447e35u;
+__constant__ uint32_t c_scan_tab[32] = {
+    // slot -> bytes 1..4 of a magic at bit offset s (blk s = 0..7, eos s = 0..7);
+    // empty slots hold a value that hashes elsewhere (never matches)
+    0x41592653u, 0x41592653u, 0x282b24cau, 0x5dc914e1u, 0xa0ac9329u, 0x50564994u, 0xbb9229c2u, 0x77245385u,
+    0x41592653u, 0x41592653u, 0x41592653u, 0x8a0ac932u, 0x41592653u, 0x41592653u, 0xee48a70au, 0x41592653u,
+    0x41592653u, 0x14159265u, 0x41592653u, 0x41592653u, 0x2ee48a70u, 0xc5056499u, 0x41592653u, 0x72453850u,
+    0x41592653u, 0x41592653u, 0x41592653u, 0xb9229c28u, 0x41592653u, 0xdc914e14u, 0x6282b24cu, 0x41592653u,
+};
+
 __global__ __launch_bounds__(256) void dec_scan_kernel(const uint8_t* __restrict__ in, uint64_t n,
                                                        DecCand* __restrict__ cand, uint32_t* __restrict__ ncand,
                                                        uint32_t cap) {
+#if BZ2MI_SCAN_HASH
+    __shared__ uint32_t htab[32];
+    if (threadIdx.x < 32) htab[threadIdx.x] = c_scan_tab[threadIdx.x];
+    __syncthreads();
+#endif
     const uint64_t wi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint64_t b0 = wi * 8;
     if (b0 >= n) return;
-    uint8_t by[20];
-#pragma unroll
-    for (int k = 0; k < 20; ++k) by[k] = (b0 + k < n) ? in[b0 + k] : 0;
     uint64_t hi = 0, lo = 0, t2 = 0;
+    if (((reinterpret_cast<uintptr_t>(in) & 3u) == 0) && b0 + 20 <= n) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(in + b0);
+        const uint32_t a0 = __builtin_bswap32(w[0]), a1 = __builtin_bswap32(w[1]), a2 = __builtin_bswap32(w[2]),
+                       a3 = __builtin_bswap32(w[3]), a4 = __builtin_bswap32(w[4]);
+        hi = ((uint64_t)a0 << 32) | a1;
+        lo = ((uint64_t)a2 << 32) | a3;
+        t2 = (uint64_t)a4 << 32;
+    } else {
+        uint8_t by[20];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) hi = (hi << 8) | by[k];
+        for (int k = 0; k < 20; ++k) by[k] = (b0 + k < n) ? in[b0 + k] : 0;
 #pragma unroll
-    for (int k = 8; k < 16; ++k) lo = (lo << 8) | by[k];
+        for (int k = 0; k < 8; ++k) hi = (hi << 8) | by[k];
 #pragma unroll
-    for (int k = 16; k < 20; ++k) t2 = (t2 << 8) | by[k];
-    t2 <<= 32;
+        for (int k = 8; k < 16; ++k) lo = (lo << 8) | by[k];
+#pragma unroll
+        for (int k = 16; k < 20; ++k) t2 = (t2 << 8) | by[k];
+        t2 <<= 32;
+    }
     // bits [q, q+64) of the 192-bit window hi:lo:t2 (q < 128)
     auto get64 = [&](int q) -> uint64_t {
         if (q == 0) return hi;
@@ -192,16 +229,31 @@ __global__ __launch_bounds__(256) void dec_scan_kernel(const uint8_t* __restrict
         return (lo << (q - 64)) | (t2 >> (128 - q));
     };
     constexpr uint64_t kBlk = 0x314159265359ull, kEos = 0x177245385090ull;
-    for (int o = 0; o < 64; ++o) {
+    auto exact = [&](int o) {
         const uint64_t p = b0 * 8 + (uint64_t)o;
-        if (p + 48 > n * 8) break;
+        if (p + 48 > n * 8) return;
         const uint64_t win = get64(o) >> 16;
         if (win == kBlk || win == kEos) {
             const uint32_t nx = (uint32_t)(get64(o + 48) >> 32);  // the 32 bits after the magic
             const uint32_t slot = atomicAdd(ncand, 1u);
             if (slot < cap) cand[slot] = DecCand{p, win == kEos ? 1u : 0u, nx};
         }
+    };
+#if BZ2MI_SCAN_HASH
+    uint32_t hits = 0;
+#pragma unroll
+    for (int B = 0; B < 8; ++B) {
+        const uint32_t v = (uint32_t)(get64(8 * (B + 1)) >> 32);  // bytes B+1..B+4
+        hits |= (htab[(v * kScanK) >> 27] == v ? 1u : 0u) << B;
     }
+    while (hits) {
+        const int B = __builtin_ctz(hits);
+        hits &= hits - 1;
+        for (int s2 = 0; s2 < 8; ++s2) exact(8 * B + s2);
+    }
+#else
+    for (int o = 0; o < 64; ++o) exact(o);
+#endif
 }
 
 // ---- K2: one wave per candidate block: header, symbol map, selectors, code
@@ -261,9 +313,18 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
         uint32_t mtf = 0x543210u;  // 4-bit entries, front = lowest nibble
         for (uint32_t i = 0; i < nsel; ++i) {
             uint32_t u = 0;
+#if BZ2MI_HUF_WORDPARSE
+            // the unary code's ones counted at once (ntab <= 6 < 8 peeked bits)
+            u = (uint32_t)__builtin_clz(~(br.peek(8) << 24) | 0x00800000u);
+            if (u < ntab) {
+                br.skip((int)u + 1);
+                br.check();
+            }
+#else
             while (br.bit()) {
                 if (++u >= ntab) break;
             }
+#endif
             if (u >= ntab || br.over) {
                 fail(info, kDecTables);
                 return;
@@ -282,10 +343,27 @@ __global__ __launch_bounds__(64) void dec_huff_kernel(const uint8_t* __restrict_
     for (uint32_t t = 0; t < ntab; ++t) {
         int cur = (int)br.bits(5);
         for (uint32_t j = 0; j < alpha; ++j) {
-            int guard = 0;
-            while (br.bit()) {
-                cur += br.bit() ? -1 : 1;
-                if (++guard > 40) break;
+#if BZ2MI_HUF_WORDPARSE
+            // "1x" pairs then a 0, read from one 32-bit peek: the first 0
+            // among the pair flags (even offsets) ends the code; each x = 1
+            // is -1, each x = 0 is +1 (more than 15 pairs: bit by bit)
+            const uint32_t w = br.peek(32);
+            const uint32_t stop = ~w & 0xAAAAAAAAu;
+            if (stop) {
+                const uint32_t kp = (uint32_t)__builtin_clz(stop) >> 1;  // pairs before the 0
+                const uint32_t top = kp ? ~0u << (32 - 2 * kp) : 0u;
+                const int xs = __popc(w & 0x55555555u & top);
+                cur += (int)kp - 2 * xs;
+                br.skip((int)(2 * kp + 1));
+                br.check();
+            } else
+#endif
+            {
+                int guard = 0;
+                while (br.bit()) {
+                    cur += br.bit() ? -1 : 1;
+                    if (++guard > 40) break;
+                }
             }
             if (cur < 1 || cur > kMaxDecLen || br.over) {
                 fail(info, kDecTables);
