@@ -235,3 +235,22 @@ def test_crafted_magics_allocate_bounded_memory(bz):
         free2, _ = torch.cuda.mem_get_info()
     used = free0 - min(free1, free2)
     assert used <= 4 * len(z) + (32 << 20), used
+
+
+def test_device_decode_unaligned_buffers(bz):
+    """Input and output device pointers at odd offsets: the input is staged
+    (the readers load 4-byte words), the RLE1 pass stores 16-byte blocks by
+    address (chunk edges byte-wise) -- the bytes around the output stay."""
+    import torch
+    from bz2mi import synth
+    data = synth.mixed_bytes(3 << 20, segment=256 << 10).tobytes()
+    z = bz.compress(data, 9, 10)
+    zin = torch.zeros(len(z) + 3, dtype=torch.uint8, device="cuda")
+    zin[3:] = torch.frombuffer(bytearray(z), dtype=torch.uint8).cuda()
+    y = torch.full((len(data) + 16,), 0xA5, dtype=torch.uint8, device="cuda")
+    with bz.Decompressor(10000) as d:
+        got = d.decompress_device(zin.data_ptr() + 3, len(z), y.data_ptr() + 5, len(data))
+    assert got == len(data)
+    out = y.cpu().numpy().tobytes()
+    assert out[5:5 + len(data)] == data
+    assert out[:5] == b"\xa5" * 5 and out[5 + len(data):] == b"\xa5" * 11
