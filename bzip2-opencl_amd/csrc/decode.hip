@@ -860,6 +860,10 @@ __global__ __launch_bounds__(64) void dec_symw_kernel(const uint8_t* __restrict_
 #ifndef BZ2MI_MTF_QUAD
 #define BZ2MI_MTF_QUAD 1
 #endif
+// BZ2MI_MTF_BFI: every quad blended with its mask, only the write predicated
+#ifndef BZ2MI_MTF_BFI
+#define BZ2MI_MTF_BFI 0
+#endif
 #ifndef BZ2MI_MTF_QGROUP
 #define BZ2MI_MTF_QGROUP 4
 #endif
@@ -1007,6 +1011,40 @@ __global__ __launch_bounds__(kDecMtfThreads) void dec_mtf_kernel(const uint16_t*
         const uint32_t wl = rr >> 2;
         const uint32_t mlast = (rr & 3) == 3 ? 0xffffffffu : ((1u << (8 * ((rr & 3) + 1))) - 1u);
 #if BZ2MI_MTF_QUAD
+#if BZ2MI_MTF_BFI
+        // quads in groups of kQG: reads in flight (unpredicated: a group
+        // never passes quad 15), then the shifts; every quad is blended with
+        // its mask (all bytes below quad ql, the partial mask at ql) and only
+        // the write is predicated
+        constexpr uint32_t kQG = BZ2MI_MTF_QGROUP;
+        static_assert(16 % kQG == 0, "groups inside the 16 quads");
+        const uint32_t ql = rr >> 4, cj = wl & 3u;
+        const uint32_t m0 = cj > 0 ? 0xffffffffu : mlast;
+        const uint32_t m1 = cj > 1 ? 0xffffffffu : cj == 1 ? mlast : 0u;
+        const uint32_t m2 = cj > 2 ? 0xffffffffu : cj == 2 ? mlast : 0u;
+        const uint32_t m3 = cj == 3 ? mlast : 0u;
+        for (uint32_t g0 = 0; g0 <= ql; g0 += kQG) {
+            uint4 o[kQG];
+#pragma unroll
+            for (uint32_t i = 0; i < kQG; ++i) o[i] = L.rec4[g0 + i][ch];
+#pragma unroll
+            for (uint32_t i = 0; i < kQG; ++i) {
+                const uint32_t q = g0 + i;
+                uint4 sh;
+                sh.x = (o[i].x << 8) | carry;
+                sh.y = __builtin_amdgcn_alignbit(o[i].y, o[i].x, 24);
+                sh.z = __builtin_amdgcn_alignbit(o[i].z, o[i].y, 24);
+                sh.w = __builtin_amdgcn_alignbit(o[i].w, o[i].z, 24);
+                carry = o[i].w >> 24;
+                const bool full = q < ql;
+                const uint32_t k0 = full ? 0xffffffffu : m0, k1 = full ? 0xffffffffu : m1;
+                const uint32_t k2 = full ? 0xffffffffu : m2, k3 = full ? 0xffffffffu : m3;
+                const uint4 nv = make_uint4((sh.x & k0) | (o[i].x & ~k0), (sh.y & k1) | (o[i].y & ~k1),
+                                            (sh.z & k2) | (o[i].z & ~k2), (sh.w & k3) | (o[i].w & ~k3));
+                if (q <= ql) L.rec4[q][ch] = nv;
+            }
+        }
+#else
         // quads in groups of kQG: reads in flight, then the shifts
         constexpr uint32_t kQG = BZ2MI_MTF_QGROUP;
         const uint32_t ql = rr >> 4, cj = wl & 3u;
@@ -1036,6 +1074,7 @@ __global__ __launch_bounds__(kDecMtfThreads) void dec_mtf_kernel(const uint16_t*
                 }
             }
         }
+#endif
 #else
         for (uint32_t g0 = 0; g0 <= wl; g0 += 8) {
             uint32_t o[8];

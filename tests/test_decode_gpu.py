@@ -254,3 +254,20 @@ def test_device_decode_unaligned_buffers(bz):
     out = y.cpu().numpy().tobytes()
     assert out[5:5 + len(data)] == data
     assert out[:5] == b"\xa5" * 5 and out[5 + len(data):] == b"\xa5" * 11
+
+
+def test_skewed_alphabet_long_codes(bz):
+    """A heavily skewed byte distribution: code lengths up to the limit
+    (codes longer than the 9-bit lookup take the windowed decoder's
+    per-symbol path) and large jumps between consecutive lengths (delta codes
+    of more than 15 pairs: the word parser's bit-by-bit fallback)."""
+    rng = np.random.default_rng(7)
+    p = 0.5 ** np.arange(1, 41)
+    p = p / p.sum()
+    sym = rng.choice(40, size=3 << 20, p=p).astype(np.uint8)
+    data = (sym * 5 + 3).astype(np.uint8).tobytes()
+    z = bz.compress(data, 9, 10)
+    with bz.Decompressor(10000) as d:
+        assert d.decompress(z) == data
+    with bz.Decompressor(100000) as d:
+        assert d.decompress(bz2.compress(data, 9)) == data
