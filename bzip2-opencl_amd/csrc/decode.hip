@@ -862,7 +862,7 @@ __global__ __launch_bounds__(64) void dec_symw_kernel(const uint8_t* __restrict_
 #endif
 // BZ2MI_MTF_BFI: every quad blended with its mask, only the write predicated
 #ifndef BZ2MI_MTF_BFI
-#define BZ2MI_MTF_BFI 0
+#define BZ2MI_MTF_BFI 1
 #endif
 #ifndef BZ2MI_MTF_QGROUP
 #define BZ2MI_MTF_QGROUP 4
